@@ -1,0 +1,1475 @@
+// rt_kernels.hip — gfx950 wavefront path tracer: kernels + the rt_abi.h C ABI.
+//
+// Reference hot path (RT/ = /root/reference/Raytracer/):
+//   render_tile            RT/raytracer.cpp:366-495   -> k_generate + k_splat
+//   advanced_integrator    RT/integrators.cpp:581-821 -> k_shade (one bounce per launch)
+//   intersect_scene        RT/intersection.cpp:606    -> k_extend
+//   intersect_shadow_ray   RT/intersection.cpp:600    -> k_connect
+//   samplers / RNG         RT/samplers.{h,cpp}        -> rt_dmath.h + sample_1d/2d below
+//   splat_filter           RT/raytracer.cpp:187-259   -> k_splat (float atomics)
+//
+// Wavefront loop: a pool of N in-flight paths lives in
+// HBM as structure-of-arrays.  One iteration = generate -> extend -> shade ->
+// connect -> splat -> bookkeep, every stage a separate kernel over a
+// compacted queue of path slots.  Queue appends are wave-aggregated
+// (__ballot + popcount + one atomic per wavefront).  Paths are regenerated
+// into freed slots every iteration so the pool stays full.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <string>
+#include <vector>
+#include <chrono>
+#include <algorithm>
+
+#include "rt_dmath.h"
+
+using namespace rtd;
+
+#define HIP_OK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { set_error(std::string(#x) + ": " + hipGetErrorString(e_)); return RT_ERROR_DEVICE; } } while (0)
+
+namespace {
+thread_local std::string g_error;
+void set_error(const std::string& s) { g_error = s; }
+bool g_profiling = false;
+uint32_t g_pool_override = 0;
+}
+
+// Tables embedded from data/ (extracted from the reference by tools/extract_tables.py).
+extern "C" const unsigned char rt_dev_strata_tab[16384];
+extern "C" const unsigned char rt_dev_bluenoise_tab[327680];
+
+// ======================================================================
+// Device scene
+// ======================================================================
+struct DevMesh { uint32_t tri_offset, node_offset, has_normals, pad; };
+
+struct DevScene {
+    const rt_material* materials;   // [material_count] + air at [material_count]
+    uint32_t material_count;
+    uint32_t air_id;
+    const rt_primitive* prims;
+    const rt_primitive* planes;
+    uint32_t plane_count;
+    const M34* inv;                 // per transform: inverse (rows 0-2)
+    const M34* fwd;                 // per transform: forward (rows 0-2)
+    const uint32_t* lights;
+    uint32_t light_count;
+    const rt_bvh_node* bvh;
+    const uint32_t* bvh_idx;
+    uint32_t bvh_node_count;
+    const DevMesh* meshes;
+    const float4* tris;             // 3 float4 per triangle: a, b-a, c-a (BVH order, all meshes)
+    const uint32_t* tri_orig;       // mesh-local original triangle index per BVH slot
+    const float* normals;           // 9 floats per triangle, ORIGINAL order (same offsets)
+    const rt_bvh_node* mnodes;      // all mesh BVH nodes (child indices mesh-local)
+    const float* sky;               // 3 floats per pixel
+    uint32_t sky_w, sky_h;
+    V3 top_sky, bot_sky;
+    const uint8_t* strata;          // g_strata_permutation_sets [256][64]
+    const uint8_t* bluenoise;       // sobol | scrambling | ranking
+};
+
+struct Ray { V3 o, d, inv_d; uint32_t neg; float max_t; };
+
+RT_D Ray make_ray(V3 o, V3 d, float far_clip) {              // RT/intersection.h:13-24
+    Ray r;
+    r.o = o; r.d = d;
+    r.inv_d = sdiv(1.0f, d);
+    r.neg = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    r.max_t = far_clip;
+    return r;
+}
+
+// ---------------------------------------------------------------- primitives
+RT_D bool ray_plane(const Ray& ray, V3 n, float d, float& t) {       // RT/intersection.cpp:12-42
+    float denom = dot(n, ray.d);
+    if (denom < -EPSILON) {
+        float tt = (d - dot(n, ray.o)) / denom;
+        if ((tt >= EPSILON) && (tt < t)) { t = tt; return true; }
+    }
+    return false;
+}
+RT_D bool ray_sphere(const Ray& ray, float r, float& t) {           // :44-74
+    V3 o = ray.o;
+    float rsq = r*r;
+    float b = dot(ray.d, o);
+    float c = dot(o, o) - rsq;
+    float discr = (b*b - c);
+    if (discr >= 0) {
+        float root = __builtin_sqrtf(discr);
+        float tn = -b - root;
+        float tf = -b + root;
+        float tt = (tn >= 0.0f ? tn : tf);
+        if ((tt >= EPSILON) && (t > tt)) { t = tt; return true; }
+    }
+    return false;
+}
+RT_D bool ray_box(const Ray& ray, V3 br, float& t) {               // :76-105
+    V3 m = ray.inv_d;
+    V3 n = mul(m, ray.o);
+    V3 k = mul(vabs(m), br);
+    V3 t1 = sub(neg(n), k);
+    V3 t2 = add(neg(n), k);
+    float tn = mx(mx(t1.x, t1.y), t1.z);
+    float tf = mn(mn(t2.x, t2.y), t2.z);
+    if (tn < tf) {
+        float tt = (tn >= 0.0f ? tn : tf);
+        if ((t > tt) && (tt >= EPSILON)) { t = tt; return true; }
+    }
+    return false;
+}
+// ray_intersect_bounding_volume (:107-133) split into the ray/box part (static)
+// and the far-clip test against the current t, done when the node is popped.
+RT_D bool bv_static(const Ray& ray, V3 p, V3 r, float& tn_out) {
+    V3 rel = sub(ray.o, p);
+    V3 m = ray.inv_d;
+    V3 n = mul(m, rel);
+    V3 k = mul(vabs(m), r);
+    V3 t1 = sub(neg(n), k);
+    V3 t2 = add(neg(n), k);
+    float tn = mx(mx(t1.x, t1.y), t1.z);
+    float tf = mn(mn(t2.x, t2.y), t2.z);
+    tn_out = tn;
+    return (tn < tf) && (tf > 0.0f);
+}
+RT_D bool ray_triangle(const Ray& ray, V3 a, V3 e1, V3 e2, float& t, float& ov, float& ow) {   // :135-182
+    const float eps = 0.000000001f;
+    V3 pvec = cross(ray.d, e2);
+    float det = dot(e1, pvec);
+    if (det > -eps && det < eps) return false;
+    float inv_det = 1.0f / det;
+    V3 tvec = sub(ray.o, a);
+    float v = dot(tvec, pvec)*inv_det;
+    if (v < 0.0f || v > 1.0f) return false;
+    V3 qvec = cross(tvec, e1);
+    float w = dot(ray.d, qvec)*inv_det;
+    if (w < 0.0f || v + w > 1.0f) return false;
+    float tt = dot(e2, qvec)*inv_det;
+    if ((tt < eps) || (t < tt)) return false;
+    t = tt; ov = v; ow = w;
+    return true;
+}
+
+RT_D M34 load_m34(const M34* p) { return *p; }
+RT_D V3 ld3(const float4& f) { return {f.x, f.y, f.z}; }
+
+RT_D void load_node(const rt_bvh_node* nodes, uint32_t i, V3& p, V3& r, uint32_t& lf, uint32_t& cnt, uint32_t& axis) {
+    const float4* q = reinterpret_cast<const float4*>(nodes + i);
+    float4 a = q[0], b = q[1];
+    p = {a.x, a.y, a.z};
+    r = {a.w, b.x, b.y};
+    lf = __float_as_uint(b.z);
+    uint32_t ca = __float_as_uint(b.w);
+    cnt = ca & 0xFFFFu;
+    axis = ca >> 16;
+}
+RT_D void load_child_boxes(const rt_bvh_node* nodes, uint32_t left, V3& p0, V3& r0, V3& p1, V3& r1) {
+    const float4* q = reinterpret_cast<const float4*>(nodes + left);
+    float4 a = q[0], b = q[1], c = q[2], d = q[3];
+    p0 = {a.x, a.y, a.z}; r0 = {a.w, b.x, b.y};
+    p1 = {c.x, c.y, c.z}; r1 = {c.w, d.x, d.y};
+}
+
+constexpr int STACK_DEPTH = 64;     // the reference's node_stack[64] (RT/intersection.cpp:261, :445)
+
+struct Hit {
+    float t;
+    uint32_t code;      // RT_HIT_MISS | RT_HIT_PLANE_BIT|plane | primitive index
+    uint32_t tri;       // global BVH-order triangle slot of the closest mesh hit
+    float v, w;         // barycentrics of that triangle (uvw = (1-v-w, v, w))
+};
+
+// Closest-hit (OCC = false) or any-hit (OCC = true) scene query:
+// intersect_scene_internal (RT/intersection.cpp:411-598) without the normal step.
+// Traversal visits nodes in exactly the reference's order (front-to-back by
+// d_is_negative[split_axis], far-clip culling against the current t at pop time),
+// so ties resolve identically.
+template <bool OCC>
+__device__ __noinline__ bool intersect(const DevScene& sc, const Ray& ray, uint32_t ignored, Hit& h) {
+    float t = ray.max_t;
+    uint32_t code = RT_HIT_MISS, tri = 0;
+    float hv = 0.0f, hw = 0.0f;
+    for (uint32_t i = 0; i < sc.plane_count; ++i) {
+        const rt_primitive& pl = sc.planes[i];
+        if (ray_plane(ray, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], t)) {
+            code = RT_HIT_PLANE_BIT | i;
+            if (OCC) { h.t = t; h.code = code; return true; }
+        }
+    }
+    uint32_t stk_node[STACK_DEPTH];
+    float stk_tn[STACK_DEPTH];
+    int sp = 0;
+    if (sc.bvh_node_count) {
+        V3 p, r; uint32_t lf, cnt, ax;
+        load_node(sc.bvh, 0, p, r, lf, cnt, ax);
+        float tn;
+        if (bv_static(ray, p, r, tn)) { stk_node[0] = 0; stk_tn[0] = tn; sp = 1; }
+    }
+    while (sp > 0) {
+        --sp;
+        uint32_t ni = stk_node[sp];
+        if (!(stk_tn[sp] < t)) continue;
+        V3 p, r; uint32_t lf, cnt, ax;
+        load_node(sc.bvh, ni, p, r, lf, cnt, ax);
+        if (cnt) {
+            for (uint32_t li = 0; li < cnt; ++li) {
+                uint32_t pi = sc.bvh_idx[lf + li];
+                if (pi == ignored) continue;
+                const rt_primitive prim = sc.prims[pi];
+                const M34 inv = load_m34(&sc.inv[prim.transform_index]);
+                Ray ir = make_ray(xform(inv, ray.o, 1.0f), xform(inv, ray.d, 0.0f), ray.max_t);   // transform_ray :403-409
+                bool hit_any = false;
+                if (prim.type == RT_PRIMITIVE_SPHERE) {
+                    hit_any = ray_sphere(ir, prim.p[0], t);
+                } else if (prim.type == RT_PRIMITIVE_BOX) {
+                    hit_any = ray_box(ir, {prim.p[0], prim.p[1], prim.p[2]}, t);
+                } else if (prim.type == RT_PRIMITIVE_MESH) {       // intersect_mesh :243-401
+                    const DevMesh mesh = sc.meshes[prim.mesh_index];
+                    const rt_bvh_node* mn_ = sc.mnodes + mesh.node_offset;
+                    uint32_t mtri = 0xFFFFFFFFu;
+                    float mv = 0.0f, mw = 0.0f;
+                    int base = sp;
+                    {
+                        V3 rp, rr; uint32_t rlf, rcnt, rax;
+                        load_node(mn_, 0, rp, rr, rlf, rcnt, rax);
+                        float tn;
+                        if (sp < STACK_DEPTH && bv_static(ir, rp, rr, tn)) { stk_node[sp] = 0; stk_tn[sp] = tn; ++sp; }
+                    }
+                    bool occluded = false;
+                    while (sp > base) {
+                        --sp;
+                        uint32_t mi = stk_node[sp];
+                        if (!(stk_tn[sp] < t)) continue;
+                        V3 np, nr; uint32_t nlf, ncnt, nax;
+                        load_node(mn_, mi, np, nr, nlf, ncnt, nax);
+                        if (ncnt) {
+                            const uint32_t g0 = mesh.tri_offset + nlf;
+                            for (uint32_t k = 0; k < ncnt; ++k) {
+                                const float4* tp = sc.tris + 3*(size_t)(g0 + k);
+                                float4 ta = tp[0], tb = tp[1], tc = tp[2];
+                                float v, w;
+                                if (ray_triangle(ir, ld3(ta), ld3(tb), ld3(tc), t, v, w)) {
+                                    if (OCC) { occluded = true; break; }
+                                    mtri = g0 + k; mv = v; mw = w;
+                                }
+                            }
+                            if (OCC && occluded) break;
+                        } else {
+                            V3 p0, r0, p1, r1;
+                            load_child_boxes(mn_, nlf, p0, r0, p1, r1);
+                            float tn0, tn1;
+                            bool h0 = bv_static(ir, p0, r0, tn0);
+                            bool h1 = bv_static(ir, p1, r1, tn1);
+                            // the reference pushes both children; the one pushed second is popped first
+                            bool left_first_pop = !((ir.neg >> nax) & 1u);
+                            if (left_first_pop) {
+                                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = nlf + 1; stk_tn[sp] = tn1; ++sp; }
+                                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = nlf; stk_tn[sp] = tn0; ++sp; }
+                            } else {
+                                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = nlf; stk_tn[sp] = tn0; ++sp; }
+                                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = nlf + 1; stk_tn[sp] = tn1; ++sp; }
+                            }
+                        }
+                    }
+                    if (OCC) {
+                        if (occluded) { h.t = t; h.code = pi; return true; }
+                    } else if (mtri != 0xFFFFFFFFu) {
+                        hit_any = true; tri = mtri; hv = mv; hw = mw;
+                    }
+                    sp = base;
+                }
+                if (hit_any) {
+                    if (OCC) { h.t = t; h.code = pi; return true; }
+                    code = pi;
+                }
+            }
+        } else {
+            V3 p0, r0, p1, r1;
+            load_child_boxes(sc.bvh, lf, p0, r0, p1, r1);
+            float tn0, tn1;
+            bool h0 = bv_static(ray, p0, r0, tn0);
+            bool h1 = bv_static(ray, p1, r1, tn1);
+            bool left_first_pop = !((ray.neg >> ax) & 1u);
+            if (left_first_pop) {
+                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = lf + 1; stk_tn[sp] = tn1; ++sp; }
+                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = lf; stk_tn[sp] = tn0; ++sp; }
+            } else {
+                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = lf; stk_tn[sp] = tn0; ++sp; }
+                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = lf + 1; stk_tn[sp] = tn1; ++sp; }
+            }
+        }
+    }
+    h.t = t; h.code = code; h.tri = tri; h.v = hv; h.w = hw;
+    return code != RT_HIT_MISS;
+}
+
+// :NormalCalculation (RT/intersection.cpp:526-591)
+RT_D void hit_geometry(const DevScene& sc, const Ray& ray, const Hit& h, V3& I, V3& N, uint32_t& material_id) {
+    I = add(ray.o, smul(h.t, ray.d));
+    V3 n = {0.0f, 0.0f, 0.0f};
+    M34 inv;
+    if (h.code & RT_HIT_PLANE_BIT) {
+        const rt_primitive& pl = sc.planes[h.code & ~RT_HIT_PLANE_BIT];
+        n = {pl.p[0], pl.p[1], pl.p[2]};
+        inv = load_m34(&sc.inv[pl.transform_index]);
+        material_id = pl.material_id;
+    } else {
+        const rt_primitive prim = sc.prims[h.code];
+        inv = load_m34(&sc.inv[prim.transform_index]);
+        material_id = prim.material_id;
+        if (prim.type == RT_PRIMITIVE_MESH) {
+            const DevMesh mesh = sc.meshes[prim.mesh_index];
+            float u = 1.0f - h.v - h.w;
+            if (mesh.has_normals) {
+                uint32_t orig = sc.tri_orig[h.tri];
+                const float* nt = sc.normals + 9*(size_t)(mesh.tri_offset + orig);
+                n = add(add(smul(u, {nt[0], nt[1], nt[2]}), smul(h.v, {nt[3], nt[4], nt[5]})),
+                        smul(h.w, {nt[6], nt[7], nt[8]}));
+            } else {
+                const float4* tp = sc.tris + 3*(size_t)h.tri;
+                V3 e1 = normalize(ld3(tp[1]));
+                V3 e2 = normalize(ld3(tp[2]));
+                n = cross(e1, e2);
+            }
+        } else {
+            V3 oo = xform(inv, ray.o, 1.0f);
+            V3 od = xform(inv, ray.d, 0.0f);
+            V3 os_p = add(oo, smul(h.t, od));
+            if (prim.type == RT_PRIMITIVE_SPHERE) {
+                n = os_p;
+            } else {
+                V3 rel = divv(os_p, {prim.p[0], prim.p[1], prim.p[2]});
+                int li = 0;
+                float le = fabsf(rel.x);
+                if (fabsf(rel.y) > le) { li = 1; le = fabsf(rel.y); }
+                if (fabsf(rel.z) > le) { li = 2; le = fabsf(rel.z); }
+                float s = sign_of(comp(rel, li));
+                n = {li == 0 ? s : 0.0f, li == 1 ? s : 0.0f, li == 2 ? s : 0.0f};
+            }
+        }
+    }
+    N = noz(xform_normal(inv, n));
+}
+
+// ======================================================================
+// Samplers (RT/samplers.cpp:18-138)
+// ======================================================================
+enum { S_DirectLighting, S_IndirectLighting, S_LightSelection, S_Reflectance, S_DOF, S_AA, S_Roulette };
+
+struct SamplerState { uint32_t x, y, index; int strategy; };
+
+RT_D float blue_noise(const uint8_t* t, int pi, int pj, int si, int dim) {   // 256spp.cpp:14-34
+    pi &= 127; pj &= 127; si &= 255; dim &= 255;
+    int ranked = si ^ (int)t[65536 + 131072 + dim + (pi + pj*128)*8];
+    int value = (int)t[dim + ranked*256];
+    value = value ^ (int)t[65536 + (dim % 8) + (pi + pj*128)*8];
+    return (float)value / 256.0f;
+}
+
+RT_D V2 sample_2d(const DevScene& sc, const SamplerState& s, Rng& rng, int dim, uint32_t bounce) {
+    int strategy = s.strategy;
+    if (strategy == RT_SAMPLING_OPTIMIZED_BLUE_NOISE && s.index > 256) strategy = RT_SAMPLING_STRATIFIED;
+    if (strategy == RT_SAMPLING_OPTIMIZED_BLUE_NOISE && dim >= 4) strategy = RT_SAMPLING_STRATIFIED;
+    float a, b, c, d;
+    unilaterals(rng, a, b, c, d);
+    (void)c; (void)d;
+    V2 r;
+    if (bounce == 0 && strategy == RT_SAMPLING_OPTIMIZED_BLUE_NOISE) {
+        float ex = (1.0f / 256.0f)*a, ey = (1.0f / 256.0f)*b;
+        r.x = ex + blue_noise(sc.bluenoise, (int)s.x, (int)s.y, (int)s.index, 2*dim);
+        r.y = ey + blue_noise(sc.bluenoise, (int)s.x, (int)s.y, (int)s.index, 2*dim + 1);
+    } else if (bounce == 0 && strategy == RT_SAMPLING_STRATIFIED) {
+        const float rx = 1.0f / 8.0f, ry = 1.0f / 8.0f;
+        uint32_t off = (73856093u*(uint32_t)dim) ^ hash_coordinate2(s.x, s.y);
+        uint32_t si = sc.strata[(off & 255u)*64u + (s.index % 64u)];
+        float sx = (float)(si % 8u)*rx, sy = (float)(si / 8u)*ry;
+        r.x = sx + a*rx; r.y = sy + b*ry;
+    } else {
+        r.x = a; r.y = b;
+    }
+    return r;
+}
+
+RT_D float sample_1d(const DevScene& sc, const SamplerState& s, Rng& rng, int dim, uint32_t bounce) {
+    int strategy = s.strategy;
+    if (strategy == RT_SAMPLING_OPTIMIZED_BLUE_NOISE && s.index > 256) strategy = RT_SAMPLING_STRATIFIED;
+    if (strategy == RT_SAMPLING_OPTIMIZED_BLUE_NOISE && dim >= 4) strategy = RT_SAMPLING_STRATIFIED;
+    float a, b, c, d;
+    unilaterals(rng, a, b, c, d);
+    (void)b; (void)c; (void)d;
+    if (bounce == 0 && strategy == RT_SAMPLING_OPTIMIZED_BLUE_NOISE) {
+        return (1.0f / 256.0f)*a + blue_noise(sc.bluenoise, (int)s.x, (int)s.y, (int)s.index, 2*dim);
+    } else if (bounce == 0 && strategy == RT_SAMPLING_STRATIFIED) {
+        const float rc = 1.0f / 64.0f;
+        uint32_t off = (73856093u*(uint32_t)dim) ^ hash_coordinate2(s.x, s.y);
+        uint32_t si = sc.strata[(off & 255u)*64u + (s.index % 64u)];
+        return (float)si*rc + a*rc;
+    }
+    return a;
+}
+
+// ======================================================================
+// Integrator helpers (RT/integrators.cpp)
+// ======================================================================
+RT_D V3 random_in_unit_sphere(Rng& e) {                                   // :11-19
+    V3 r;
+    do {
+        float a, b, c, d;
+        unilaterals(e, a, b, c, d);
+        r = {a*2.0f - 1.0f, b*2.0f - 1.0f, c*2.0f - 1.0f};
+    } while (length_sq(r) >= 1.0f);
+    return r;
+}
+RT_D V3 oriented_around_normal(V3 v, V3 n) {                             // :58-75
+    float sign = copy_sign(1.0f, n.z);
+    float a = -1.0f / (sign + n.z);
+    float b = n.x*n.y*a;
+    V3 T = {1.0f + sign*n.x*n.x*a, sign*b, -sign*n.x};
+    V3 B = {b, sign + n.y*n.y*a, -n.y};
+    return add(add(smul(v.x, B), smul(v.y, n)), smul(v.z, T));
+}
+RT_D V3 map_to_hemisphere(V3 N, V2 rs) {                                 // :93-105
+    float az = TAU_32*rs.x, y = rs.y;
+    float s = __builtin_sqrtf(1.0f - y*y);
+    V3 h = {d_cosf(az)*s, y, d_sinf(az)*s};
+    return oriented_around_normal(h, N);
+}
+RT_D V3 map_to_cosine_weighted_hemisphere(V3 N, V2 rs) {                 // :107-119
+    float az = TAU_32*rs.x, y = rs.y;
+    float s = __builtin_sqrtf(1.0f - y);
+    V3 h = {d_cosf(az)*s, __builtin_sqrtf(y), d_sinf(az)*s};
+    return oriented_around_normal(h, N);
+}
+RT_D float fresnel_dielectric(float ci, float ei, float et, float eta, float& co) {   // :235-258
+    float si = __builtin_sqrtf(mx(0.0f, 1.0f - ci*ci));
+    float st = eta*si;
+    float ct = __builtin_sqrtf(mx(0.0f, 1.0f - st*st));
+    co = ct;
+    if (st >= 1) return 1;
+    float rpar = (((et*ci) - (ei*ct)) / ((et*ci) + (ei*ct)));
+    float rperp = (((ei*ci) - (et*ct)) / ((ei*ci) + (et*ct)));
+    return 0.5f * (rpar * rpar + rperp * rperp);
+}
+RT_D V3 sample_sky(const DevScene& sc, V3 d) {                           // :272-295
+    if (sc.sky) {
+        float rcp_pi = 1.0f / PI_32;
+        float rcp_2pi = 0.5f / PI_32;
+        float phi = d_atan2f(d.z, d.x);
+        float theta = d_asinf(d.y);
+        float u = 0.5f + rcp_2pi*phi;
+        float v = 0.5f + rcp_pi*theta;
+        uint32_t sx = (uint32_t)(int32_t)(u*(float)sc.sky_w) % sc.sky_w;
+        uint32_t sy = (uint32_t)(int32_t)(v*(float)sc.sky_h) % sc.sky_h;
+        const float* p = sc.sky + 3*((size_t)sy*sc.sky_w + sx);
+        return {p[0], p[1], p[2]};
+    }
+    return lerp3(sc.bot_sky, sc.top_sky, fabsf(d.y));
+}
+RT_D V3 evaluate_material(const rt_material& m, V3 p) {                 // :297-308
+    if (m.flags & RT_MATERIAL_CHECKERS) {
+        int32_t ch = (((int32_t)floorf(0.25f*p.x)) ^ ((int32_t)floorf(0.25f*p.z))) & 1;
+        if (ch) return {m.checker_color.x, m.checker_color.y, m.checker_color.z};
+    }
+    return {m.albedo.x, m.albedo.y, m.albedo.z};
+}
+__host__ __device__ inline V3 rv3(const rt_v3& a) { return {a.x, a.y, a.z}; }
+RT_D V3 translation(const M34& m) { return {m.e[0][3], m.e[1][3], m.e[2][3]}; }
+
+// pick_random_light (:135-192) without scratch arrays: one pass for the sum,
+// a second for the CDF walk (identical additions, identical rounding).
+RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float rs, V3 I, float& out_p) {
+    uint32_t n = sc.light_count;
+    if (n == 0) return 0;
+    if (st.importance_sample_lights) {
+        float sum = 0.0f;
+        for (uint32_t i = 0; i < n; ++i) {
+            const rt_primitive light = sc.prims[sc.lights[i]];
+            V3 lv = sub(translation(sc.fwd[light.transform_index]), I);
+            float dsq = length_sq(lv);
+            float l = max3(rv3(sc.materials[light.material_id].emission_color));
+            float psa = light.type == RT_PRIMITIVE_SPHERE ? PI_32*light.p[0]*light.p[0] / dsq : 0.0f;
+            sum += l*psa;
+        }
+        float e = sum*rs;
+        float cdf = 0.0f, pdf = 0.0f;
+        uint32_t li = 0;
+        for (; li < n; ++li) {
+            const rt_primitive light = sc.prims[sc.lights[li]];
+            V3 lv = sub(translation(sc.fwd[light.transform_index]), I);
+            float dsq = length_sq(lv);
+            float l = max3(rv3(sc.materials[light.material_id].emission_color));
+            float psa = light.type == RT_PRIMITIVE_SPHERE ? PI_32*light.p[0]*light.p[0] / dsq : 0.0f;
+            pdf = l*psa;
+            cdf = (li > 0 ? cdf : 0.0f) + pdf;
+            if (!(cdf < e) || li == n - 1) break;
+        }
+        out_p = pdf / sum;
+        return sc.lights[li];
+    }
+    out_p = 1.0f / (float)n;
+    float f = rs*(float)n - EPSILON;
+    uint32_t li = f <= 0.0f ? 0u : (uint32_t)f;
+    if (li >= n) li = n - 1;
+    return sc.lights[li];
+}
+
+// ======================================================================
+// Path pool (SoA in HBM)
+// ======================================================================
+struct Pool {
+    uint32_t n;
+    float4* ray_o;       // o.xyz | w: pixel index bits
+    float4* ray_d;       // d.xyz | w: sample offset bits
+    float4* thr;         // throughput.xyz | w: vignette
+    float4* L;           // total_color.xyz | w: flags bits (bounce 0-7, specular 8, stack_at 9-15)
+    float4* prev_n;      // prev_N.xyz | w: unused
+    float2* jitter;
+    uint4*  rng;
+    float4* hit;         // t | code | tri | v
+    float*  hit_w;
+    uint16_t* mstack;    // [64][n]
+    uint32_t* ext_q[2];
+    uint32_t* done_q;
+    uint32_t* free_q;
+    uint32_t* sh_slot;
+    float4*   sh_o;      // o.xyz | w: light id bits
+    float4*   sh_d;      // d.xyz | w: max_t
+    float4*   sh_c;      // contribution.xyz
+};
+
+struct Counters {
+    uint32_t ext_count[2];
+    uint32_t shadow_count;
+    uint32_t done_count;
+    uint32_t free_count;
+    uint32_t freed;
+    uint32_t cancel;
+    uint32_t pad;
+    unsigned long long next_sample;
+    unsigned long long total_samples;
+    unsigned long long closest_rays;
+    unsigned long long shadow_rays;
+};
+
+struct FrameParams {
+    uint32_t w, h, frame_count, total_frame_index;
+    uint32_t tile_w, tile_h, tcx;
+    uint32_t pixels;                // P: pixels owned by this shard
+    uint32_t ntiles;
+    const uint32_t* tile_ids;       // owned tiles
+    const uint32_t* tile_prefix;    // [ntiles+1] pixel prefix sums
+    // explicit sample list mode (rt_trace_samples)
+    const uint32_t* list_xy;
+    const uint32_t* list_s;
+    float* list_out;
+    // camera (RT/raytracer.cpp:381-401)
+    V3 cp, cx, cy, cz;
+    float focus_distance, lens_radius, half_film_w, half_film_h, film_distance;
+    // filter
+    const float* lut;               // 512 floats
+    int32_t kernel_size, cache_size;
+    float4* accum;
+};
+
+// wave-aggregated queue append: one atomic per wavefront
+RT_D uint32_t wave_append(uint32_t* counter, bool pred) {
+    unsigned long long mask = __ballot(pred);
+    if (mask == 0ull) return 0;
+    uint32_t lane = __lane_id();
+    uint32_t leader = (uint32_t)__ffsll((long long)mask) - 1u;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, (int)leader);
+    unsigned long long lower = mask & ((1ull << lane) - 1ull);
+    return base + (uint32_t)__popcll(lower);
+}
+
+RT_D uint32_t n_new_paths(const Counters* c) {
+    unsigned long long remaining = c->total_samples - c->next_sample;
+    return (uint32_t)(remaining < (unsigned long long)c->free_count ? remaining : c->free_count);
+}
+
+// ---- lens (RT/raytracer.cpp:86-123)
+RT_D V2 transform_bokeh_sample(V2 o, float f, float n, float phi_shutter_max) {
+    V2 ab = {(o.x*2.0f) - 1.0f, (o.y*2.0f) - 1.0f};
+    V2 phir;
+    if ((ab.x*ab.x) > (ab.y*ab.y)) {
+        phir.x = (fabsf(ab.x) > 1e-8f) ? ((PI_32*0.25f)*(ab.y / ab.x)) : 0.0f;
+        phir.y = ab.x;
+    } else {
+        phir.x = (fabsf(ab.y) > 1e-8f) ? ((PI_32*0.5f) - ((PI_32*0.25f)*(ab.x / ab.y))) : 0.0f;
+        phir.y = ab.y;
+    }
+    phir.x += f*phi_shutter_max;
+    if (f > 0.0f) {
+        float k = floorf(((n*phir.x) + PI_32) / (2.0f*PI_32));
+        phir.y *= d_powf(d_cosf(PI_32 / n) / d_cosf(phir.x - ((2.0f*(PI_32 / n))*k)), f);
+    } else {
+        phir.y *= 1.0f;
+    }
+    return {d_cosf(phir.x)*phir.y, d_sinf(phir.x)*phir.y};
+}
+RT_D V2 brown_conrady(V2 uv, float amount, float woh) {
+    uv.y /= woh;
+    float bd1 = 0.1f*amount, bd2 = -0.025f*amount;
+    float r2 = uv.x*uv.x + uv.y*uv.y;
+    float f = 1.0f + r2*bd1 + r2*r2*bd2;
+    uv.x *= f; uv.y *= f;
+    uv.y *= woh;
+    return uv;
+}
+RT_D void apply_lens_distortion(float amount, uint32_t w, uint32_t h, float& u, float& v) {
+    float woh = (float)w / (float)h;
+    V2 mn_ = brown_conrady({0.0f, 0.0f}, amount, woh);
+    V2 mx_ = brown_conrady({1.0f, 1.0f}, amount, woh);
+    V2 uv = brown_conrady({u, v}, amount, woh);
+    if (amount > 0.0f) {
+        uv.x = (uv.x - mn_.x) / (mn_.x + mx_.x);
+        uv.y = (uv.y - mn_.y) / (mn_.y + mx_.y);
+    }
+    u = uv.x; v = uv.y;
+}
+
+RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return bounce | (spec << 8) | (at << 9); }
+
+// ======================================================================
+// Kernels
+// ======================================================================
+constexpr int BLOCK = 256;
+
+// k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
+__global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
+                                                    Counters* cnt, int cur) {
+    const uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
+    const uint32_t n_new = n_new_paths(cnt);
+    const bool active = i < n_new;
+    uint32_t slot = 0;
+    bool enqueue = false;
+    if (active) {
+        slot = pool.free_q[cnt->free_count - 1u - i];
+        unsigned long long k = cnt->next_sample + i;
+        uint32_t x, y, s;
+        if (fp.list_xy) {
+            x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
+        } else {
+            uint32_t pass = (uint32_t)(k / fp.pixels);
+            uint32_t p = (uint32_t)(k % fp.pixels);
+            uint32_t lo = 0, hi = fp.ntiles;                 // tile_prefix[lo] <= p < tile_prefix[lo+1]
+            while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (fp.tile_prefix[mid] <= p) lo = mid; else hi = mid; }
+            uint32_t tile = fp.tile_ids[lo];
+            uint32_t local = p - fp.tile_prefix[lo];
+            uint32_t min_x = fp.tile_w*(tile % fp.tcx), min_y = fp.tile_h*(tile / fp.tcx);
+            uint32_t tw = min(fp.w, min_x + fp.tile_w) - min_x;
+            x = min_x + local % tw; y = min_y + local / tw; s = pass;
+        }
+        uint32_t canonical = fp.frame_count + s;
+        uint32_t tile = (y / fp.tile_h)*fp.tcx + (x / fp.tile_w);
+        Rng rng = random_seed(sample_seed(fp.total_frame_index, fp.frame_count, tile, y*fp.w + x, canonical));
+        // camera (RT/raytracer.cpp:381-401)
+        float hfw = fp.half_film_w*fp.focus_distance;
+        float hfh = fp.half_film_h*fp.focus_distance;
+        float film_distance = fp.focus_distance*fp.film_distance;
+        V3 film_center = sub(fp.cp, smul(film_distance, fp.cz));
+        float pixel_w = 1.0f / (float)fp.w, pixel_h = 1.0f / (float)fp.h;
+        float v = 1.0f - 2.0f*(float)y*pixel_h;
+        float u = 1.0f - 2.0f*(float)x*pixel_w;
+        apply_lens_distortion(st.lens_distortion, fp.w, fp.h, u, v);
+        SamplerState ss = {x, y, canonical, st.sampling_strategy};
+        V2 aa = sample_2d(sc, ss, rng, S_AA, 0);
+        float jx = aa.x - 0.5f, jy = aa.y - 0.5f;
+        V2 dof = sample_2d(sc, ss, rng, S_DOF, 0);
+        dof = transform_bokeh_sample(dof, st.f_factor, st.diaphragm_edges, PI_32*st.phi_shutter_max);
+        float djx = hfw*pixel_w*fp.lens_radius*dof.x;
+        float djy = hfh*pixel_h*fp.lens_radius*dof.y;
+        V3 film_p = film_center;
+        film_p = add(film_p, smul((u + pixel_w*jx)*hfw, fp.cx));
+        film_p = add(film_p, smul((v + pixel_h*jy)*hfh, fp.cy));
+        V3 jcp = add(add(fp.cp, smul(djx, fp.cx)), smul(djy, fp.cy));
+        V3 rd = normalize(sub(film_p, jcp));
+        float vig = dot(rd, fp.cz);
+        vig = vig*vig*vig*vig;
+        vig = lerpf_(1.0f, vig, st.vignette_strength);
+        pool.ray_o[slot] = make_float4(jcp.x, jcp.y, jcp.z, __uint_as_float(y*fp.w + x));
+        pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
+        pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
+        pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(pack_flags(0, 1, 0)));
+        pool.prev_n[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        pool.jitter[slot] = make_float2(jx, jy);
+        pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
+        pool.mstack[slot] = (uint16_t)sc.air_id;            // material_stack[0] = &air
+        enqueue = st.max_bounce_count > 0;
+    }
+    // new paths go to the current extension queue behind the survivors of the last shade
+    uint32_t pos = wave_append(&cnt->ext_count[cur], active && enqueue);
+    if (active && enqueue) pool.ext_q[cur][pos] = slot;
+    uint32_t dpos = wave_append(&cnt->done_count, active && !enqueue);
+    if (active && !enqueue) pool.done_q[dpos] = slot;
+}
+
+// k_extend — intersect_scene for every queued path (RT/intersection.cpp:606-610)
+__global__ void __launch_bounds__(BLOCK) k_extend(DevScene sc, Pool pool, const Counters* cnt, int cur) {
+    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
+    if (q >= cnt->ext_count[cur]) return;
+    const uint32_t slot = pool.ext_q[cur][q];
+    float4 o = pool.ray_o[slot], d = pool.ray_d[slot];
+    Ray ray = make_ray(ld3(o), ld3(d), FLT_MAX_);
+    Hit h;
+    intersect<false>(sc, ray, 0, h);
+    pool.hit[slot] = make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v);
+    pool.hit_w[slot] = h.w;
+}
+
+// k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
+__global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
+                                                 Counters* cnt, int cur) {
+    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
+    const bool valid = q < cnt->ext_count[cur];
+    bool cont = false, done = false, shadow = false;
+    uint32_t slot = 0;
+    V3 sh_o = {0, 0, 0}, sh_d = {0, 0, 0}, sh_c = {0, 0, 0};
+    float sh_t = 0.0f;
+    uint32_t sh_light = 0;
+    if (valid) {
+        slot = pool.ext_q[cur][q];
+        const float4 o4 = pool.ray_o[slot], d4 = pool.ray_d[slot];
+        const float4 t4 = pool.thr[slot], L4 = pool.L[slot], pn4 = pool.prev_n[slot];
+        const float4 h4 = pool.hit[slot];
+        const uint4 r4 = pool.rng[slot];
+        Rng rng = {r4.x, r4.y, r4.z, r4.w};
+        V3 ro = ld3(o4), rd = ld3(d4);
+        V3 thr = ld3(t4), total = ld3(L4), prev_N = ld3(pn4);
+        uint32_t flags = __float_as_uint(L4.w);
+        uint32_t bounce = flags & 0xFFu, is_spec = (flags >> 8) & 1u;
+        int32_t at = (int32_t)((flags >> 9) & 0x7Fu);
+        uint32_t pixel = __float_as_uint(o4.w);
+        uint32_t sample_off = __float_as_uint(d4.w);
+        uint32_t px = pixel % fp.w, py = pixel / fp.w;
+        uint32_t canonical = fp.frame_count + (fp.list_xy ? fp.list_s[sample_off] : sample_off);
+        SamplerState ss = {px, py, canonical, st.sampling_strategy};
+        Hit h;
+        h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = pool.hit_w[slot];
+        Ray ray; ray.o = ro; ray.d = rd;
+        if (h.code != RT_HIT_MISS) {
+            V3 I, N;
+            uint32_t surf_id;
+            hit_geometry(sc, ray, h, I, N, surf_id);
+            float t = h.t;
+            float cos_i = -dot(rd, N);
+            bool inside = (cos_i < 0.0f);
+            uint32_t mi_id, mt_id;
+            if (inside) {
+                mi_id = surf_id;
+                mt_id = pool.mstack[(size_t)(at - 1 > 0 ? at - 1 : 0)*pool.n + slot];
+                cos_i = -cos_i;
+                N = neg(N);
+            } else {
+                mi_id = pool.mstack[(size_t)at*pool.n + slot];
+                mt_id = surf_id;
+            }
+            const rt_material mi = sc.materials[mi_id];
+            const rt_material mt = sc.materials[mt_id];
+            if (mi.is_participating_medium) {                                  // Beer :640-649
+                V3 ab = {d_expf(-mi.absorb.x*t), d_expf(-mi.absorb.y*t), d_expf(-mi.absorb.z*t)};
+                thr = mul(thr, ab);
+            }
+            if (mt.flags & RT_MATERIAL_EMISSIVE) {                             // :651-670
+                bool allow = (!st.next_event_estimation ||
+                              ((st.caustics || (bounce < 2)) && is_spec));
+                if (allow) {
+                    total = add(total, mul(thr, rv3(mt.emission_color)));
+                } else if (bounce > 0 && st.use_mis) {
+                    float ldsq = t*t;
+                    float light_pdf = ldsq / cos_i;
+                    float brdf_pdf = (st.importance_sample_diffuse ? dot(prev_N, rd) / PI_32 : 1.0f / (2.0f*PI_32));
+                    float mis_pdf = light_pdf + brdf_pdf;
+                    total = add(total, mul(smul(1.0f / mis_pdf, thr), rv3(mt.emission_color)));
+                }
+                done = true;
+            } else {
+                float eta_i = mi.ior, eta_t = mt.ior;
+                float eta = eta_i / eta_t;
+                float cos_t;
+                float refl = fresnel_dielectric(cos_i, eta_i, eta_t, eta, cos_t);
+                float reflect_test = sample_1d(sc, ss, rng, S_Reflectance, bounce);
+                refl = lerpf_(refl, 1.0f, mt.metallic);
+                is_spec = 1;
+                if (reflect_test < refl) {                                      // reflect :684-696
+                    V3 nd = reflect(rd, N);
+                    if (mt.roughness > 0.0f) {
+                        V3 rs = random_in_unit_sphere(rng);
+                        nd = normalize(add(smul(1.0f + EPSILON, nd), smul(mt.roughness, rs)));
+                    }
+                    ro = add(I, smul(EPSILON, nd)); rd = nd;
+                    thr = mul(thr, lerp3(v3s(1.0f), rv3(mt.albedo), mt.metallic));
+                } else if (mt.is_participating_medium) {                       // refract :698-717
+                    if (inside) {
+                        if (at > 0) --at;
+                    } else if (at < 63) {
+                        ++at;
+                        pool.mstack[(size_t)at*pool.n + slot] = (uint16_t)mt_id;
+                    }
+                    V3 fd = add(smul(eta, rd), muls(N, (eta*cos_i - cos_t)));
+                    ro = add(I, muls(fd, EPSILON)); rd = fd;
+                } else {                                                        // diffuse :718-790
+                    is_spec = 0;
+                    V3 albedo = evaluate_material(mt, I);
+                    V3 brdf = smul(1.0f / PI_32, albedo);
+                    if (st.next_event_estimation && sc.light_count > 0) {      // NEE :738-771
+                        float lps = sample_1d(sc, ss, rng, S_LightSelection, bounce);
+                        float lrp = 0.0f;
+                        uint32_t lid = pick_random_light(sc, st, lps, I, lrp);
+                        const rt_primitive light = sc.prims[lid];
+                        V2 s2 = sample_2d(sc, ss, rng, S_DirectLighting, bounce);
+                        // random_point_on_light (:199-228), sphere lights
+                        const M34 lf = load_m34(&sc.fwd[light.transform_index]);
+                        V3 towards = normalize(sub(translation(lf), I));
+                        if (light.type == RT_PRIMITIVE_SPHERE) {
+                            float rad = light.p[0];
+                            V3 Nl = map_to_hemisphere(neg(towards), s2);
+                            V3 pw = xform(lf, muls(Nl, rad), 1.0f);
+                            V3 Lv = sub(pw, I);
+                            float dsq = length_sq(Lv);
+                            float dist = __builtin_sqrtf(dsq);
+                            Lv = divs(Lv, dist);
+                            float A = 2.0f*PI_32*rad*rad;
+                            float ndl = dot(N, Lv);
+                            float nndl = -dot(Nl, Lv);
+                            if (ndl > 0.0f && nndl > 0.0f) {
+                                float sa = (nndl * A) / dsq;
+                                float pdf;
+                                if (st.use_mis) {
+                                    float lpdf = 1.0f / sa;
+                                    float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
+                                    pdf = lpdf + bpdf;
+                                } else {
+                                    pdf = 1.0f / sa;
+                                }
+                                pdf *= lrp;
+                                sh_c = mul(mul(muls(thr, dot(N, Lv) / pdf), brdf),
+                                           rv3(sc.materials[light.material_id].emission_color));
+                                sh_o = add(I, muls(Lv, EPSILON));
+                                sh_d = Lv;
+                                sh_t = dist - 2*EPSILON;
+                                sh_light = lid;
+                                shadow = true;
+                            }
+                        }
+                    }
+                    V2 s2 = sample_2d(sc, ss, rng, S_IndirectLighting, bounce); // indirect :777-789
+                    V3 R;
+                    if (st.importance_sample_diffuse) {
+                        R = map_to_cosine_weighted_hemisphere(N, s2);
+                        thr = muls(thr, PI_32);
+                    } else {
+                        R = map_to_hemisphere(N, s2);
+                        thr = muls(thr, 2.0f*PI_32*dot(N, R));
+                    }
+                    thr = mul(thr, brdf);
+                    ro = add(I, muls(N, EPSILON)); rd = R;
+                }
+                if (st.russian_roulette && !is_spec) {                          // RR :801-811
+                    float p = clampf_(max3(thr), 0.1f, 0.9f);
+                    float e = sample_1d(sc, ss, rng, S_Roulette, bounce);
+                    if (e > p) done = true;
+                    else thr = muls(thr, 1.0f / p);
+                }
+            }
+            if (!done) {
+                prev_N = N;
+                ++bounce;
+                if (bounce >= st.max_bounce_count) done = true;
+            }
+        } else {
+            total = add(total, mul(thr, sample_sky(sc, rd)));                 // miss :812-815
+            done = true;
+        }
+        cont = !done;
+        pool.ray_o[slot] = make_float4(ro.x, ro.y, ro.z, o4.w);
+        pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, d4.w);
+        pool.thr[slot] = make_float4(thr.x, thr.y, thr.z, t4.w);
+        pool.L[slot] = make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at)));
+        pool.prev_n[slot] = make_float4(prev_N.x, prev_N.y, prev_N.z, 0.0f);
+        pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
+    }
+    const int nxt = cur ^ 1;
+    uint32_t pos = wave_append(&cnt->ext_count[nxt], cont);
+    if (cont) pool.ext_q[nxt][pos] = slot;
+    uint32_t spos = wave_append(&cnt->shadow_count, shadow);
+    if (shadow) {
+        pool.sh_slot[spos] = slot;
+        pool.sh_o[spos] = make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light));
+        pool.sh_d[spos] = make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t);
+        pool.sh_c[spos] = make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f);
+    }
+    uint32_t dpos = wave_append(&cnt->done_count, done);
+    if (done) pool.done_q[dpos] = slot;
+}
+
+// k_connect — intersect_shadow_ray (RT/integrators.cpp:756, RT/intersection.cpp:600-604)
+__global__ void __launch_bounds__(BLOCK) k_connect(DevScene sc, Pool pool, const Counters* cnt) {
+    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
+    if (q >= cnt->shadow_count) return;
+    const float4 o = pool.sh_o[q], d = pool.sh_d[q];
+    Ray ray = make_ray(ld3(o), ld3(d), d.w);
+    Hit h;
+    if (!intersect<true>(sc, ray, __float_as_uint(o.w), h)) {
+        const uint32_t slot = pool.sh_slot[q];
+        const float4 c = pool.sh_c[q];
+        float4 L = pool.L[slot];
+        L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;
+        pool.L[slot] = L;
+    }
+}
+
+// k_splat — vignette + splat_filter (RT/raytracer.cpp:469-488, 187-259) with
+// float atomics, then the slot returns to the free list.
+__global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Counters* cnt) {
+    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
+    const bool valid = q < cnt->done_count;
+    uint32_t slot = 0;
+    if (valid) {
+        slot = pool.done_q[q];
+        const float4 L = pool.L[slot];
+        const float vig = pool.thr[slot].w;
+        const float2 j = pool.jitter[slot];
+        V3 r = muls(ld3(L), vig);
+        const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
+        if (fp.list_xy) {
+            const uint32_t k = __float_as_uint(pool.ray_d[slot].w);
+            float* o = fp.list_out + 5*(size_t)k;
+            o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = j.x; o[4] = j.y;
+        } else if (fp.cache_size) {
+            const int64_t x = pixel % fp.w, y = pixel / fp.w;
+            const int64_t ks = fp.kernel_size;
+            const float kscale = (float)(fp.cache_size - 1) / (float)ks;
+            int64_t x0 = x - ks, x1 = x + ks + 1, y0 = y - ks, y1 = y + ks + 1;
+            int64_t xm = 0, ym = 0;
+            if (x0 < 0) { xm = -x0; x0 = 0; }
+            if (y0 < 0) { ym = -y0; y0 = 0; }
+            if (x1 > (int64_t)fp.w) x1 = fp.w;
+            if (y1 > (int64_t)fp.h) y1 = fp.h;
+            for (int64_t sy = y0; sy < y1; ++sy) {
+                int32_t jy = (int32_t)fabsf(0.5f + kscale*((float)(ym + (sy - y0) - ks) - j.y));
+                float fy = fp.lut[jy];
+                for (int64_t sx = x0; sx < x1; ++sx) {
+                    int32_t jx = (int32_t)fabsf(0.5f + kscale*((float)(xm + (sx - x0) - ks) - j.x));
+                    float f = fp.lut[jx]*fy;
+                    float* dst = reinterpret_cast<float*>(fp.accum + (size_t)sy*fp.w + sx);
+                    unsafeAtomicAdd(dst + 0, f*r.x);
+                    unsafeAtomicAdd(dst + 1, f*r.y);
+                    unsafeAtomicAdd(dst + 2, f*r.z);
+                    unsafeAtomicAdd(dst + 3, f);
+                }
+            }
+        } else {
+            float* dst = reinterpret_cast<float*>(fp.accum + pixel);
+            unsafeAtomicAdd(dst + 0, r.x);
+            unsafeAtomicAdd(dst + 1, r.y);
+            unsafeAtomicAdd(dst + 2, r.z);
+            unsafeAtomicAdd(dst + 3, 1.0f);
+        }
+    }
+    // free the slot: positions after the ones generate consumed this iteration
+    uint32_t pos = wave_append(&cnt->freed, valid);
+    if (valid) pool.free_q[cnt->free_count - n_new_paths(cnt) + pos] = slot;
+}
+
+// k_bookkeep — end of iteration: counters roll over (single thread)
+__global__ void k_bookkeep(Counters* cnt, int cur) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t n_new = n_new_paths(cnt);
+    cnt->closest_rays += cnt->ext_count[cur];
+    cnt->shadow_rays += cnt->shadow_count;
+    cnt->free_count = cnt->free_count - n_new + cnt->freed;
+    cnt->next_sample += n_new;
+    cnt->freed = 0;
+    cnt->ext_count[cur] = 0;
+    cnt->shadow_count = 0;
+    cnt->done_count = 0;
+}
+
+__global__ void k_init_free(uint32_t* free_q, uint32_t n) {
+    uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
+    if (i < n) free_q[i] = n - 1u - i;       // slot 0 handed out first
+}
+
+// debug / parity kernel: intersect_scene / intersect_shadow_ray for explicit rays
+__global__ void k_debug_intersect(DevScene sc, const rt_ray_query* rays, rt_hit_record* out, uint32_t n, int occ) {
+    uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    rt_ray_query rq = rays[i];
+    Ray ray = make_ray(rv3(rq.o), rv3(rq.d), rq.max_t);
+    Hit h;
+    rt_hit_record r;
+    memset(&r, 0, sizeof(r));
+    bool hit = occ ? intersect<true>(sc, ray, rq.ignored_primitive, h) : intersect<false>(sc, ray, rq.ignored_primitive, h);
+    r.t = h.t;
+    r.primitive = hit ? h.code : RT_HIT_MISS;
+    if (hit && !occ) {
+        V3 I, N; uint32_t mid;
+        hit_geometry(sc, ray, h, I, N, mid);
+        r.hit_p = {I.x, I.y, I.z};
+        r.n = {N.x, N.y, N.z};
+    }
+    out[i] = r;
+}
+
+// ======================================================================
+// Host side: rt_scene + C ABI
+// ======================================================================
+struct rt_scene {
+    int device = 0;
+    DevScene ds = {};
+    std::vector<void*> allocs;
+    // render-time state (grown on demand)
+    Pool pool = {};
+    std::vector<void*> pool_allocs;
+    Counters* cnt = nullptr;
+    Counters* cnt_host = nullptr;       // pinned
+    uint32_t* d_tiles = nullptr;
+    size_t tiles_cap = 0;
+    float* d_lut = nullptr;
+    volatile int cancel = 0;
+    uint32_t bvh_depth = 0;
+    hipEvent_t ev[2 * RT_KERNEL_COUNT] = {};
+    bool events = false;
+};
+
+namespace {
+
+template <typename T>
+int upload(rt_scene* s, const T* host, size_t count, const T** out) {
+    *out = nullptr;
+    if (!count) return RT_OK;
+    void* p = nullptr;
+    HIP_OK(hipMalloc(&p, sizeof(T)*count));
+    s->allocs.push_back(p);
+    HIP_OK(hipMemcpy(p, host, sizeof(T)*count, hipMemcpyHostToDevice));
+    *out = static_cast<const T*>(p);
+    return RT_OK;
+}
+
+uint32_t tree_depth(const rt_bvh_node* nodes, uint32_t count) {
+    if (!count) return 0;
+    uint32_t maxd = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> st{{0u, 1u}};
+    while (!st.empty()) {
+        auto [n, d] = st.back(); st.pop_back();
+        maxd = std::max(maxd, d);
+        if (n >= count) continue;
+        const rt_bvh_node& nd = nodes[n];
+        if (!nd.count && !(n == 0 && nd.left_first == 0)) {
+            if (nd.left_first + 1 >= count) continue;
+            st.push_back({nd.left_first, d + 1});
+            st.push_back({nd.left_first + 1, d + 1});
+        }
+    }
+    return maxd;
+}
+
+void free_pool(rt_scene* s) {
+    for (void* p : s->pool_allocs) (void)hipFree(p);
+    s->pool_allocs.clear();
+    s->pool = Pool{};
+}
+
+int ensure_pool(rt_scene* s, uint32_t n) {
+    if (s->pool.n >= n) return RT_OK;
+    free_pool(s);
+    Pool& p = s->pool;
+    auto alloc = [&](void** ptr, size_t bytes) -> int {
+        HIP_OK(hipMalloc(ptr, bytes));
+        s->pool_allocs.push_back(*ptr);
+        return RT_OK;
+    };
+    int e = 0;
+    size_t N = n;
+    e |= alloc((void**)&p.ray_o, 16*N);
+    e |= alloc((void**)&p.ray_d, 16*N);
+    e |= alloc((void**)&p.thr, 16*N);
+    e |= alloc((void**)&p.L, 16*N);
+    e |= alloc((void**)&p.prev_n, 16*N);
+    e |= alloc((void**)&p.jitter, 8*N);
+    e |= alloc((void**)&p.rng, 16*N);
+    e |= alloc((void**)&p.hit, 16*N);
+    e |= alloc((void**)&p.hit_w, 4*N);
+    e |= alloc((void**)&p.mstack, 2*64*N);
+    e |= alloc((void**)&p.ext_q[0], 4*N);
+    e |= alloc((void**)&p.ext_q[1], 4*N);
+    e |= alloc((void**)&p.done_q, 4*N);
+    e |= alloc((void**)&p.free_q, 4*N);
+    e |= alloc((void**)&p.sh_slot, 4*N);
+    e |= alloc((void**)&p.sh_o, 16*N);
+    e |= alloc((void**)&p.sh_d, 16*N);
+    e |= alloc((void**)&p.sh_c, 16*N);
+    if (e) { free_pool(s); return RT_ERROR_OUT_OF_MEMORY; }
+    p.n = n;
+    return RT_OK;
+}
+
+int check_inputs(const rt_settings* st, const rt_filter_cache* f) {
+    if (!st || !f) { set_error("null settings/filter"); return RT_ERROR_INVALID; }
+    if (st->integrator != RT_INTEGRATOR_ADVANCED) { set_error("only the Advanced Pathtracer integrator is on the device path"); return RT_ERROR_INVALID; }
+    if (st->max_bounce_count > 63) { set_error("max_bounce_count > 63 overruns the 64-entry material stack"); return RT_ERROR_INVALID; }
+    if (st->use_path_guide) { set_error("use_path_guide is dead code in the reference and unsupported"); return RT_ERROR_INVALID; }
+    if (st->sampling_strategy < 0 || st->sampling_strategy > 2) { set_error("bad sampling_strategy"); return RT_ERROR_INVALID; }
+    if (f->cache_size && (f->kernel_size == 0 || f->kernel_size > 32 || f->cache_size > 256)) { set_error("bad filter cache"); return RT_ERROR_INVALID; }
+    return RT_OK;
+}
+
+// The wavefront driver shared by rt_render_device and rt_trace_samples.
+int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long long total, hipStream_t stream, rt_stats* stats) {
+    auto t0 = std::chrono::steady_clock::now();
+    uint32_t pool_n = g_pool_override ? g_pool_override : (1u << 21);
+    if ((unsigned long long)pool_n > total) pool_n = (uint32_t)std::max<unsigned long long>(total, 1ull);
+    pool_n = (pool_n + BLOCK - 1) / BLOCK * BLOCK;
+    int err = ensure_pool(s, pool_n);
+    if (err) return err;
+    Pool pool = s->pool;
+    const uint32_t N = pool.n;
+    Counters init = {};
+    init.free_count = N;
+    init.total_samples = total;
+    HIP_OK(hipMemcpyAsync(s->cnt, &init, sizeof(Counters), hipMemcpyHostToDevice, stream));
+    k_init_free<<<(N + BLOCK - 1) / BLOCK, BLOCK, 0, stream>>>(pool.free_q, N);
+    HIP_OK(hipGetLastError());
+    const uint32_t grid = (N + BLOCK - 1) / BLOCK;
+    double kms[RT_KERNEL_COUNT] = {};
+    uint64_t klaunch[RT_KERNEL_COUNT] = {};
+    const bool prof = g_profiling;
+    if (prof && !s->events) {
+        for (auto& e : s->ev) HIP_OK(hipEventCreate(&e));
+        s->events = true;
+    }
+    auto stage_begin = [&](int k) { if (prof) (void)hipEventRecord(s->ev[2*k], stream); };
+    auto stage_end = [&](int k) {
+        if (!prof) return;
+        (void)hipEventRecord(s->ev[2*k + 1], stream);
+        (void)hipEventSynchronize(s->ev[2*k + 1]);
+        float ms = 0.0f;
+        (void)hipEventElapsedTime(&ms, s->ev[2*k], s->ev[2*k + 1]);
+        kms[k] += ms; klaunch[k] += 1;
+    };
+    s->cancel = 0;
+    uint64_t iters = 0;
+    int cur = 0;
+    for (;;) {
+        stage_begin(RT_KERNEL_GENERATE);
+        k_generate<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
+        stage_end(RT_KERNEL_GENERATE);
+        stage_begin(RT_KERNEL_EXTEND);
+        k_extend<<<grid, BLOCK, 0, stream>>>(s->ds, pool, s->cnt, cur);
+        stage_end(RT_KERNEL_EXTEND);
+        stage_begin(RT_KERNEL_SHADE);
+        k_shade<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
+        stage_end(RT_KERNEL_SHADE);
+        stage_begin(RT_KERNEL_CONNECT);
+        k_connect<<<grid, BLOCK, 0, stream>>>(s->ds, pool, s->cnt);
+        stage_end(RT_KERNEL_CONNECT);
+        stage_begin(RT_KERNEL_SPLAT);
+        k_splat<<<grid, BLOCK, 0, stream>>>(fp, pool, s->cnt);
+        stage_end(RT_KERNEL_SPLAT);
+        k_bookkeep<<<1, 64, 0, stream>>>(s->cnt, cur);
+        HIP_OK(hipGetLastError());
+        ++iters;
+        cur ^= 1;
+        if ((iters & 3u) == 0u || iters < 4) {
+            HIP_OK(hipMemcpyAsync(s->cnt_host, s->cnt, sizeof(Counters), hipMemcpyDeviceToHost, stream));
+            HIP_OK(hipStreamSynchronize(stream));
+            const Counters& c = *s->cnt_host;
+            if (c.next_sample >= c.total_samples && c.ext_count[cur] == 0) break;
+            if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
+            if (iters > 100000) { set_error("wavefront loop did not converge"); return RT_ERROR_DEVICE; }
+        }
+    }
+    HIP_OK(hipMemcpyAsync(s->cnt_host, s->cnt, sizeof(Counters), hipMemcpyDeviceToHost, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        stats->closest_hit_rays = s->cnt_host->closest_rays;
+        stats->shadow_rays = s->cnt_host->shadow_rays;
+        stats->samples = total;
+        stats->iterations = iters;
+        stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (int k = 0; k < RT_KERNEL_COUNT; ++k) { stats->kernel_ms[k] = kms[k]; stats->kernel_launches[k] = klaunch[k]; }
+    }
+    return RT_OK;
+}
+
+void fill_camera(FrameParams& fp, const rt_camera* c) {
+    fp.cp = rv3(c->p); fp.cx = rv3(c->x); fp.cy = rv3(c->y); fp.cz = rv3(c->z);
+    fp.focus_distance = c->focus_distance;
+    fp.lens_radius = c->lens_radius;
+    fp.half_film_w = c->half_film_w;
+    fp.half_film_h = c->half_film_h;
+    fp.film_distance = c->film_distance;
+}
+
+int bind_device(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+        set_error("no HIP device visible: the MI355X path has no CPU fallback");
+        return RT_ERROR_NO_DEVICE;
+    }
+    if (device < 0 || device >= count) { set_error("device index out of range"); return RT_ERROR_INVALID; }
+    HIP_OK(hipSetDevice(device));
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+const char* rt_last_error(void) { return g_error.c_str(); }
+
+int rt_device_count(int* out) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    if (out) *out = n;
+    return RT_OK;
+}
+
+int rt_set_profiling(int enable) { g_profiling = enable != 0; return RT_OK; }
+int rt_set_path_pool(uint32_t paths) { g_pool_override = paths; return RT_OK; }
+
+int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
+    if (!d || !out) { set_error("null argument"); return RT_ERROR_INVALID; }
+    *out = nullptr;
+    int err = bind_device(device);
+    if (err) return err;
+    if (d->material_count == 0 || d->material_count >= 0xFFFFu) { set_error("material count must be in [1, 65534]"); return RT_ERROR_INVALID; }
+    rt_scene* s = new rt_scene();
+    s->device = device;
+    DevScene& ds = s->ds;
+    auto fail = [&](int e) { rt_scene_free(s); return e; };
+    // materials + the integrator's local `air` (RT/integrators.cpp:597-599)
+    std::vector<rt_material> mats(d->materials, d->materials + d->material_count);
+    rt_material air = {};
+    air.ior = 1.0f;
+    air.is_participating_medium = 1;
+    mats.push_back(air);
+    ds.material_count = d->material_count;
+    ds.air_id = d->material_count;
+    if ((err = upload(s, mats.data(), mats.size(), &ds.materials))) return fail(err);
+    for (uint32_t i = 0; i < d->primitive_count; ++i) {
+        const rt_primitive& p = d->primitives[i];
+        if (p.transform_index >= d->transform_count || p.material_id >= d->material_count ||
+            (p.type == RT_PRIMITIVE_MESH && p.mesh_index >= d->mesh_count)) {
+            set_error("primitive references out of range"); return fail(RT_ERROR_INVALID);
+        }
+    }
+    for (uint32_t i = 0; i < d->plane_count; ++i)
+        if (d->planes[i].transform_index >= d->transform_count || d->planes[i].material_id >= d->material_count) {
+            set_error("plane references out of range"); return fail(RT_ERROR_INVALID);
+        }
+    for (uint32_t i = 0; i < d->light_count; ++i)
+        if (d->lights[i] >= d->primitive_count) { set_error("light id out of range"); return fail(RT_ERROR_INVALID); }
+    if ((err = upload(s, d->primitives, d->primitive_count, &ds.prims))) return fail(err);
+    if ((err = upload(s, d->planes, d->plane_count, &ds.planes))) return fail(err);
+    ds.plane_count = d->plane_count;
+    std::vector<M34> inv(d->transform_count), fwd(d->transform_count);
+    for (uint32_t i = 0; i < d->transform_count; ++i)
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 4; ++c) { inv[i].e[r][c] = d->transforms[i].inverse.e[r][c]; fwd[i].e[r][c] = d->transforms[i].forward.e[r][c]; }
+    if ((err = upload(s, inv.data(), inv.size(), &ds.inv))) return fail(err);
+    if ((err = upload(s, fwd.data(), fwd.size(), &ds.fwd))) return fail(err);
+    if ((err = upload(s, d->lights, d->light_count, &ds.lights))) return fail(err);
+    ds.light_count = d->light_count;
+    uint32_t top_depth = tree_depth(d->bvh_nodes, d->bvh_node_count);
+    for (uint32_t i = 0; i < d->bvh_index_count; ++i)
+        if (d->bvh_indices[i] >= d->primitive_count) { set_error("bvh index out of range"); return fail(RT_ERROR_INVALID); }
+    if ((err = upload(s, d->bvh_nodes, d->bvh_node_count, &ds.bvh))) return fail(err);
+    if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
+    ds.bvh_node_count = d->bvh_node_count;
+    // meshes: concatenate, triangles as (a, b-a, c-a) float4 triples
+    std::vector<DevMesh> meshes(d->mesh_count);
+    std::vector<float4> tris;
+    std::vector<uint32_t> orig;
+    std::vector<float> normals;
+    std::vector<rt_bvh_node> mnodes;
+    uint32_t mesh_depth = 0;
+    for (uint32_t m = 0; m < d->mesh_count; ++m) {
+        const rt_mesh& M = d->meshes[m];
+        meshes[m].tri_offset = (uint32_t)orig.size();
+        meshes[m].node_offset = (uint32_t)mnodes.size();
+        meshes[m].has_normals = (M.has_normals && M.normals) ? 1u : 0u;
+        for (uint32_t i = 0; i < M.node_count; ++i) {
+            const rt_bvh_node& nd = M.nodes[i];
+            if (nd.count ? (nd.left_first + nd.count > M.triangle_count) : (nd.left_first + 1 >= M.node_count && !(i == 0 && nd.left_first == 0))) {
+                set_error("mesh BVH node out of range"); return fail(RT_ERROR_INVALID);
+            }
+        }
+        mesh_depth = std::max(mesh_depth, tree_depth(M.nodes, M.node_count));
+        for (uint32_t t = 0; t < M.triangle_count; ++t) {
+            const rt_v3* v = M.triangles + 3*(size_t)t;
+            tris.push_back(make_float4(v[0].x, v[0].y, v[0].z, 0.0f));
+            tris.push_back(make_float4(v[1].x - v[0].x, v[1].y - v[0].y, v[1].z - v[0].z, 0.0f));
+            tris.push_back(make_float4(v[2].x - v[0].x, v[2].y - v[0].y, v[2].z - v[0].z, 0.0f));
+            if (M.indices[t] >= M.triangle_count) { set_error("mesh index out of range"); return fail(RT_ERROR_INVALID); }
+            orig.push_back(M.indices[t]);
+        }
+        for (uint32_t t = 0; t < M.triangle_count; ++t)
+            for (int k = 0; k < 3; ++k) {
+                rt_v3 nn = meshes[m].has_normals ? M.normals[3*(size_t)t + k] : rt_v3{0, 0, 0};
+                normals.push_back(nn.x); normals.push_back(nn.y); normals.push_back(nn.z);
+            }
+        mnodes.insert(mnodes.end(), M.nodes, M.nodes + M.node_count);
+    }
+    if (top_depth + mesh_depth + 2 > STACK_DEPTH) {
+        set_error("BVH too deep for the 64-entry traversal stack (RT/intersection.cpp:445)");
+        return fail(RT_ERROR_INVALID);
+    }
+    s->bvh_depth = top_depth + mesh_depth;
+    if ((err = upload(s, meshes.data(), meshes.size(), &ds.meshes))) return fail(err);
+    if ((err = upload(s, tris.data(), tris.size(), &ds.tris))) return fail(err);
+    if ((err = upload(s, orig.data(), orig.size(), &ds.tri_orig))) return fail(err);
+    if ((err = upload(s, normals.data(), normals.size(), &ds.normals))) return fail(err);
+    if ((err = upload(s, mnodes.data(), mnodes.size(), &ds.mnodes))) return fail(err);
+    if (d->skydome && d->skydome_w && d->skydome_h) {
+        if ((err = upload(s, reinterpret_cast<const float*>(d->skydome), 3*(size_t)d->skydome_w*d->skydome_h, &ds.sky))) return fail(err);
+        ds.sky_w = d->skydome_w; ds.sky_h = d->skydome_h;
+    }
+    ds.top_sky = rv3(d->top_sky_color);
+    ds.bot_sky = rv3(d->bot_sky_color);
+    if ((err = upload(s, rt_dev_strata_tab, sizeof(rt_dev_strata_tab), &ds.strata))) return fail(err);
+    if ((err = upload(s, rt_dev_bluenoise_tab, sizeof(rt_dev_bluenoise_tab), &ds.bluenoise))) return fail(err);
+    if (hipMalloc(&s->cnt, sizeof(Counters)) != hipSuccess) { set_error("hipMalloc counters"); return fail(RT_ERROR_OUT_OF_MEMORY); }
+    if (hipHostMalloc(&s->cnt_host, sizeof(Counters)) != hipSuccess) { set_error("hipHostMalloc"); return fail(RT_ERROR_OUT_OF_MEMORY); }
+    if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
+    *out = s;
+    return RT_OK;
+}
+
+int rt_scene_free(rt_scene* s) {
+    if (!s) return RT_OK;
+    (void)hipSetDevice(s->device);
+    for (void* p : s->allocs) (void)hipFree(p);
+    free_pool(s);
+    if (s->cnt) (void)hipFree(s->cnt);
+    if (s->cnt_host) (void)hipHostFree(s->cnt_host);
+    if (s->d_tiles) (void)hipFree(s->d_tiles);
+    if (s->d_lut) (void)hipFree(s->d_lut);
+    if (s->events) for (auto& e : s->ev) (void)hipEventDestroy(e);
+    delete s;
+    return RT_OK;
+}
+
+int rt_cancel(rt_scene* s) { if (s) s->cancel = 1; return RT_OK; }
+
+int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st,
+                     const rt_filter_cache* filter, const rt_tile_set* tiles,
+                     uint32_t total_frame_index, uint32_t w, uint32_t h, uint32_t frame_count,
+                     float* d_pixels, void* hip_stream, rt_stats* stats) {
+    if (!s || !camera || !tiles || !d_pixels || !w || !h) { set_error("null argument"); return RT_ERROR_INVALID; }
+    int err = check_inputs(st, filter);
+    if (err) return err;
+    if (!tiles->tile_w || !tiles->tile_h || !tiles->shard_count || tiles->shard_index >= tiles->shard_count) {
+        set_error("bad tile set"); return RT_ERROR_INVALID;
+    }
+    HIP_OK(hipSetDevice(s->device));
+    hipStream_t stream = (hipStream_t)hip_stream;
+    FrameParams fp = {};
+    fp.w = w; fp.h = h; fp.frame_count = frame_count; fp.total_frame_index = total_frame_index;
+    fp.tile_w = tiles->tile_w; fp.tile_h = tiles->tile_h;
+    fp.tcx = (w + tiles->tile_w - 1) / tiles->tile_w;
+    uint32_t tcy = (h + tiles->tile_h - 1) / tiles->tile_h;
+    // owned tiles: t % shard_count == shard_index, descending like the reference's queue (:555)
+    std::vector<uint32_t> ids, prefix(1, 0);
+    for (uint32_t t = fp.tcx*tcy; t-- > 0;) {
+        if (t % tiles->shard_count != tiles->shard_index) continue;
+        uint32_t min_x = tiles->tile_w*(t % fp.tcx), min_y = tiles->tile_h*(t / fp.tcx);
+        uint32_t tw = std::min(w, min_x + tiles->tile_w) - min_x, th = std::min(h, min_y + tiles->tile_h) - min_y;
+        ids.push_back(t);
+        prefix.push_back(prefix.back() + tw*th);
+    }
+    if (ids.empty()) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
+    size_t need = ids.size() + prefix.size();
+    if (s->tiles_cap < need) {
+        if (s->d_tiles) (void)hipFree(s->d_tiles);
+        s->d_tiles = nullptr;
+        HIP_OK(hipMalloc(&s->d_tiles, need*sizeof(uint32_t)));
+        s->tiles_cap = need;
+    }
+    std::vector<uint32_t> packed(ids);
+    packed.insert(packed.end(), prefix.begin(), prefix.end());
+    HIP_OK(hipMemcpyAsync(s->d_tiles, packed.data(), packed.size()*sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    HIP_OK(hipMemcpyAsync(s->d_lut, filter->cache, 512*sizeof(float), hipMemcpyHostToDevice, stream));
+    fp.ntiles = (uint32_t)ids.size();
+    fp.tile_ids = s->d_tiles;
+    fp.tile_prefix = s->d_tiles + ids.size();
+    fp.pixels = prefix.back();
+    fill_camera(fp, camera);
+    fp.lut = s->d_lut;
+    fp.kernel_size = (int32_t)filter->kernel_size;
+    fp.cache_size = (int32_t)filter->cache_size;
+    fp.accum = reinterpret_cast<float4*>(d_pixels);
+    unsigned long long total = (unsigned long long)fp.pixels*st->samples_per_pixel;
+    if (total == 0) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
+    return run_frame(s, st, fp, total, stream, stats);
+}
+
+int rt_render(rt_scene* s, const rt_camera* camera, const rt_settings* st, const rt_filter_cache* filter,
+              const rt_tile_set* tiles, uint32_t total_frame_index, rt_accumulation_buffer* accum, rt_stats* stats) {
+    if (!s || !accum || !accum->pixels) { set_error("null argument"); return RT_ERROR_INVALID; }
+    HIP_OK(hipSetDevice(s->device));
+    size_t bytes = (size_t)accum->w*accum->h*4*sizeof(float);
+    float* d = nullptr;
+    HIP_OK(hipMalloc(&d, bytes));
+    int err = RT_OK;
+    if (hipMemcpy(d, accum->pixels, bytes, hipMemcpyHostToDevice) != hipSuccess) { set_error("copy in"); err = RT_ERROR_DEVICE; }
+    if (!err) err = rt_render_device(s, camera, st, filter, tiles, total_frame_index, accum->w, accum->h,
+                                     accum->frame_count, d, nullptr, stats);
+    if (!err && hipMemcpy(accum->pixels, d, bytes, hipMemcpyDeviceToHost) != hipSuccess) { set_error("copy out"); err = RT_ERROR_DEVICE; }
+    (void)hipFree(d);
+    return err;
+}
+
+int rt_trace_samples(rt_scene* s, const rt_camera* camera, const rt_settings* st,
+                     uint32_t w, uint32_t h, uint32_t tile_w, uint32_t tile_h,
+                     uint32_t frame_count, uint32_t total_frame_index,
+                     uint32_t count, const uint32_t* pixel_xy, const uint32_t* sample_offset,
+                     float* out, rt_stats* stats) {
+    rt_filter_cache box = {};
+    int err = check_inputs(st, &box);
+    if (err) return err;
+    if (!s || !camera || !pixel_xy || !sample_offset || !out || !w || !h || !tile_w || !tile_h) { set_error("null argument"); return RT_ERROR_INVALID; }
+    if (!count) return RT_OK;
+    for (uint32_t i = 0; i < count; ++i)
+        if (pixel_xy[2*i] >= w || pixel_xy[2*i + 1] >= h) { set_error("sample pixel out of range"); return RT_ERROR_INVALID; }
+    HIP_OK(hipSetDevice(s->device));
+    uint32_t* d_xy = nullptr; uint32_t* d_s = nullptr; float* d_out = nullptr;
+    HIP_OK(hipMalloc(&d_xy, 8*(size_t)count));
+    HIP_OK(hipMalloc(&d_s, 4*(size_t)count));
+    HIP_OK(hipMalloc(&d_out, 20*(size_t)count));
+    HIP_OK(hipMemcpy(d_xy, pixel_xy, 8*(size_t)count, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_s, sample_offset, 4*(size_t)count, hipMemcpyHostToDevice));
+    FrameParams fp = {};
+    fp.w = w; fp.h = h; fp.frame_count = frame_count; fp.total_frame_index = total_frame_index;
+    fp.tile_w = tile_w; fp.tile_h = tile_h; fp.tcx = (w + tile_w - 1) / tile_w;
+    fp.list_xy = d_xy; fp.list_s = d_s; fp.list_out = d_out;
+    fill_camera(fp, camera);
+    err = run_frame(s, st, fp, count, nullptr, stats);
+    if (!err && hipMemcpy(out, d_out, 20*(size_t)count, hipMemcpyDeviceToHost) != hipSuccess) { set_error("copy out"); err = RT_ERROR_DEVICE; }
+    (void)hipFree(d_xy); (void)hipFree(d_s); (void)hipFree(d_out);
+    return err;
+}
+
+int rt_debug_intersect(rt_scene* s, uint32_t count, const rt_ray_query* rays, int occlusion, rt_hit_record* out) {
+    if (!s || !rays || !out) { set_error("null argument"); return RT_ERROR_INVALID; }
+    if (!count) return RT_OK;
+    HIP_OK(hipSetDevice(s->device));
+    rt_ray_query* d_r = nullptr; rt_hit_record* d_o = nullptr;
+    HIP_OK(hipMalloc(&d_r, sizeof(rt_ray_query)*count));
+    HIP_OK(hipMalloc(&d_o, sizeof(rt_hit_record)*count));
+    HIP_OK(hipMemcpy(d_r, rays, sizeof(rt_ray_query)*count, hipMemcpyHostToDevice));
+    k_debug_intersect<<<(count + 127) / 128, 128>>>(s->ds, d_r, d_o, count, occlusion);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpy(out, d_o, sizeof(rt_hit_record)*count, hipMemcpyDeviceToHost));
+    (void)hipFree(d_r); (void)hipFree(d_o);
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,285 @@
+/*
+ * rt_abi.h — C ABI of the MI355X wavefront path tracer (drop-in for the
+ * reference's tile renderer hot path).
+ *
+ * The reference (TheSandvichMaker/BUAS-Pathtracer) renders a frame as
+ *   render_all_tiles (RT/raytracer.cpp:692)
+ *     -> worker threads -> try_render_next_tile (:551)
+ *       -> render_tile (:366) -> per pixel, per sample:
+ *            scene->settings.integrator->f(&state)   (:467, advanced_integrator
+ *                                                     RT/integrators.cpp:581-821)
+ *            splat_filter(...)                       (:187-259)
+ * into an AccumulationBuffer{w,h,frame_count,V4* pixels} (RT/Raytracer.h:44-48).
+ *
+ * Per-sample function pointers are far too fine-grained for a GPU, so this
+ * ABI replaces the path at frame / tile-set granularity:
+ * rt_render() consumes the same Scene / Material / Camera / SceneSettings /
+ * FilterCache data (flattened to plain arrays: pointers become indices) and
+ * fills the same float4 accumulation buffer.
+ *
+ * Everything here is plain C: POD structs, pointers and sizes, no C++ or
+ * torch types.  Every function returns an int status (RT_OK == 0); on error
+ * rt_last_error() returns a thread-local message.
+ *
+ * RT/ = /root/reference/Raytracer/,  MathLib/ = /root/reference/MathLib/.
+ */
+#ifndef RT_ABI_H
+#define RT_ABI_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+enum rt_status {
+    RT_OK                 = 0,
+    RT_ERROR_INVALID      = 1,  /* bad argument / unsupported setting      */
+    RT_ERROR_DEVICE       = 2,  /* HIP runtime failure                     */
+    RT_ERROR_OUT_OF_MEMORY= 3,
+    RT_ERROR_CANCELLED    = 4,  /* rt_cancel() hit during rt_render()      */
+    RT_ERROR_NO_DEVICE    = 5,  /* no MI355X visible: the product path never
+                                   falls back to a CPU implementation      */
+};
+
+/* ------------------------------------------------------------ math types */
+typedef struct rt_v3 { float x, y, z; } rt_v3;                 /* MathLib/math_types.h:12-17 */
+typedef struct rt_m4x4 { float e[4][4]; } rt_m4x4;             /* MathLib/math_types.h:43-45 */
+typedef struct rt_m4x4inv { rt_m4x4 forward, inverse; } rt_m4x4inv; /* :47-50 */
+
+/* ----------------------------------------------------------- scene model */
+enum rt_material_flag {                                        /* RT/scene.h:9-13 */
+    RT_MATERIAL_MIRROR   = 0x1,
+    RT_MATERIAL_CHECKERS = 0x2,
+    RT_MATERIAL_EMISSIVE = 0x4,
+};
+
+typedef struct rt_material {                                   /* RT/scene.h:15-29 (68 B) */
+    uint32_t flags;
+    rt_v3    albedo;
+    rt_v3    checker_color;
+    rt_v3    emission_color;
+    float    ior;
+    float    metallic;
+    float    roughness;
+    int32_t  is_participating_medium;
+    rt_v3    absorb;                                           /* Medium::absorb */
+} rt_material;
+
+enum rt_primitive_type {                                       /* RT/primitives.h:3-10 */
+    RT_PRIMITIVE_NONE   = 0,
+    RT_PRIMITIVE_PLANE  = 1,
+    RT_PRIMITIVE_SPHERE = 2,
+    RT_PRIMITIVE_BOX    = 3,
+    RT_PRIMITIVE_MESH   = 4,
+};
+
+typedef struct rt_primitive {                                  /* RT/primitives.h:92-106 */
+    uint32_t transform_index;  /* Primitive::transform -> index into transforms[] */
+    uint32_t material_id;      /* MaterialID */
+    uint32_t type;             /* rt_primitive_type */
+    uint32_t mesh_index;       /* RT_PRIMITIVE_MESH: index into meshes[] */
+    float    p[4];             /* plane: n.xyz, d | sphere: r | box: r.xyz */
+} rt_primitive;
+
+typedef struct rt_bvh_node {                                   /* RT/bvh.h:31-37 (32 B) */
+    rt_v3    bv_p;             /* centre      */
+    rt_v3    bv_r;             /* half extent */
+    uint32_t left_first;       /* interior: left child (right = +1); leaf: first index */
+    uint16_t count;            /* > 0 => leaf */
+    uint16_t split_axis;
+} rt_bvh_node;
+
+typedef struct rt_mesh {               /* RT/primitives.h:58-67 + MeshBVH RT/bvh.h:52-58 */
+    uint32_t            triangle_count;
+    uint32_t            has_normals;
+    const rt_v3*        triangles;  /* MeshBVH::triangles: BVH order, a,b,c per triangle */
+    const uint32_t*     indices;    /* MeshBVH::indices: BVH slot -> original triangle  */
+    const rt_v3*        normals;    /* get_normals(mesh): ORIGINAL order, 3 per triangle */
+    uint32_t            node_count;
+    const rt_bvh_node*  nodes;      /* BVHStorage_Scalar layout (node 1 is padding)      */
+} rt_mesh;
+
+typedef struct rt_scene_desc {                                 /* RT/scene.h:92-120 */
+    uint32_t            material_count;   const rt_material*  materials;  /* [0] null material  */
+    uint32_t            primitive_count;  const rt_primitive* primitives; /* [0] null primitive */
+    uint32_t            plane_count;      const rt_primitive* planes;     /* Scene::planes      */
+    uint32_t            transform_count;  const rt_m4x4inv*   transforms;
+    uint32_t            light_count;      const uint32_t*     lights;     /* PrimitiveIDs       */
+    uint32_t            mesh_count;       const rt_mesh*      meshes;
+    uint32_t            bvh_node_count;   const rt_bvh_node*  bvh_nodes;  /* Scene::bvh         */
+    uint32_t            bvh_index_count;  const uint32_t*     bvh_indices;
+    rt_v3               top_sky_color;
+    rt_v3               bot_sky_color;
+    uint32_t            skydome_w, skydome_h;
+    const rt_v3*        skydome;          /* EnvironmentMap pixels (Image_V3), NULL = sky colours */
+} rt_scene_desc;
+
+typedef struct rt_camera {                                     /* RT/scene.h:31-46 */
+    rt_v3 p, x, y, z;
+    float vfov;
+    float aspect_ratio;
+    float lens_radius;
+    float focus_distance;
+    float film_distance;
+    float half_film_w;
+    float half_film_h;
+} rt_camera;
+
+enum rt_sampling_strategy {                                    /* RT/samplers.h:110-117 */
+    RT_SAMPLING_UNIFORM              = 0,
+    RT_SAMPLING_OPTIMIZED_BLUE_NOISE = 1,
+    RT_SAMPLING_STRATIFIED           = 2,
+};
+
+enum rt_integrator {                                           /* g_integrators RT/integrators.cpp:823 */
+    RT_INTEGRATOR_ADVANCED = 0,   /* "Advanced Pathtracer" — the only one on the hot path */
+};
+
+typedef struct rt_settings {                                   /* RT/scene.h:64-82 */
+    int32_t  next_event_estimation;
+    int32_t  importance_sample_lights;
+    int32_t  importance_sample_diffuse;
+    int32_t  use_mis;
+    int32_t  russian_roulette;
+    int32_t  caustics;
+    int32_t  sampling_strategy;     /* rt_sampling_strategy */
+    int32_t  use_path_guide;        /* must be 0 (dead code in the reference) */
+    float    vignette_strength;
+    float    lens_distortion;
+    float    f_factor;
+    float    diaphragm_edges;
+    float    phi_shutter_max;
+    uint32_t samples_per_pixel;
+    uint32_t max_bounce_count;      /* <= 63: the material stack holds 64 entries */
+    int32_t  integrator;            /* rt_integrator (SceneSettings::integrator) */
+} rt_settings;
+
+typedef struct rt_filter_cache {                               /* FilterCache RT/Raytracer.h:34-40 */
+    uint32_t kernel_size;           /* filter radius in pixels; 0 => box (plain accumulate) */
+    uint32_t cache_size;            /* 256 when a kernel is loaded, 0 for the box filter    */
+    float    cache[512];            /* load_reconstruction_kernel RT/raytracer.cpp:164-185 */
+} rt_filter_cache;
+
+typedef struct rt_accumulation_buffer {                        /* RT/Raytracer.h:44-48 */
+    uint32_t w, h;
+    uint32_t frame_count;
+    float*   pixels;                /* w*h float4 (xyz = weighted radiance, w = weight) */
+} rt_accumulation_buffer;
+
+typedef struct rt_tile_set {        /* WorkQueue tiling RT/Raytracer.h:70-91 + sharding */
+    uint32_t tile_w, tile_h;        /* 64x64 in the reference (RT/raytracer.cpp:1657) */
+    uint32_t shard_index;           /* this GPU renders tiles t with t % shard_count == shard_index */
+    uint32_t shard_count;
+} rt_tile_set;
+
+enum rt_rng_mode {
+    /* One xorshift RandomSeries per sample, seeded from
+     * (total_frame_index, frame_count, tile_index, pixel, sample): the draw
+     * order inside a sample is exactly the reference's.  The GPU path. */
+    RT_RNG_PER_SAMPLE  = 0,
+    /* One RandomSeries per 64x64 tile consumed serially in pixel/sample order,
+     * exactly RT/raytracer.cpp:588-593 (CPU oracle only). */
+    RT_RNG_TILE_STREAM = 1,
+};
+
+enum rt_kernel_id {                 /* wavefront stages, for rt_stats::kernel_ms */
+    RT_KERNEL_GENERATE = 0,         /* camera rays (render_tile ray setup)               */
+    RT_KERNEL_EXTEND   = 1,         /* closest hit (intersect_scene)                     */
+    RT_KERNEL_SHADE    = 2,         /* one bounce of advanced_integrator                 */
+    RT_KERNEL_CONNECT  = 3,         /* shadow rays (intersect_shadow_ray)                */
+    RT_KERNEL_SPLAT    = 4,         /* splat_filter into the accumulation buffer         */
+    RT_KERNEL_COUNT    = 6,
+};
+
+typedef struct rt_stats {
+    uint64_t closest_hit_rays;      /* intersect_scene calls (RT/integrators.cpp:615)      */
+    uint64_t shadow_rays;           /* intersect_shadow_ray calls (RT/integrators.cpp:756) */
+    uint64_t samples;               /* camera samples integrated                            */
+    uint64_t iterations;            /* wavefront iterations (GPU) / 0 (CPU)                 */
+    double   seconds;               /* wall time of the render call                         */
+    /* filled only while rt_set_profiling(1): HIP-event time per stage, summed over
+       launches, measured on the stream the stage kernels run on */
+    double   kernel_ms[RT_KERNEL_COUNT];
+    uint64_t kernel_launches[RT_KERNEL_COUNT];
+} rt_stats;
+
+typedef struct rt_ray_query {       /* debug/parity entry: one ray for rt_debug_intersect */
+    rt_v3    o, d;
+    float    max_t;
+    uint32_t ignored_primitive;     /* 0 for closest hit; light id for shadow rays */
+} rt_ray_query;
+
+typedef struct rt_hit_record {
+    float    t;
+    uint32_t primitive;             /* primitive index, or RT_HIT_PLANE_BIT|plane index; 0xFFFFFFFF = miss */
+    rt_v3    hit_p;
+    rt_v3    n;
+} rt_hit_record;
+
+#define RT_HIT_MISS       0xFFFFFFFFu
+#define RT_HIT_PLANE_BIT  0x80000000u
+
+/* ------------------------------------------------------------ functions */
+typedef struct rt_scene rt_scene;   /* device-resident scene (opaque) */
+
+int         rt_abi_version(void);
+const char* rt_last_error(void);
+int         rt_device_count(int* out_count);
+
+/* Upload a flattened scene to `device` (create_scene_bvh must have run on
+ * the host: RT/scene.cpp:173-242).  The device copy is owned by *out. */
+int rt_scene_upload(const rt_scene_desc* desc, int device, rt_scene** out);
+int rt_scene_free(rt_scene* scene);
+
+/* Render one progressive frame: the equivalent of render_all_tiles releasing
+ * its workers over every tile of `tiles` (RT/raytracer.cpp:692-757), with
+ * accum->frame_count as the canonical sample base (RT/raytracer.cpp:427-428).
+ * accum->pixels is HOST memory; samples are ADDED to it (the caller resets it
+ * exactly as reset() does, RT/raytracer.cpp:511-515). */
+int rt_render(rt_scene* scene, const rt_camera* camera, const rt_settings* settings,
+              const rt_filter_cache* filter, const rt_tile_set* tiles,
+              uint32_t total_frame_index, rt_accumulation_buffer* accum, rt_stats* stats);
+
+/* Same, but d_pixels is a DEVICE pointer (w*h float4 on the scene's device)
+ * and `hip_stream` (hipStream_t, may be NULL) is the stream the work is
+ * ordered on.  Returns after the frame has completed on the device. */
+int rt_render_device(rt_scene* scene, const rt_camera* camera, const rt_settings* settings,
+                     const rt_filter_cache* filter, const rt_tile_set* tiles,
+                     uint32_t total_frame_index, uint32_t w, uint32_t h, uint32_t frame_count,
+                     float* d_pixels, void* hip_stream, rt_stats* stats);
+
+/* Parity entry: integrate an explicit list of samples (pixel x,y + sample
+ * offset s, canonical index = frame_count + s) with RT_RNG_PER_SAMPLE and
+ * return, per sample, {r, g, b, jitter_x, jitter_y} (radiance after
+ * vignetting, the value splat_filter receives).  Host pointers. */
+int rt_trace_samples(rt_scene* scene, const rt_camera* camera, const rt_settings* settings,
+                     uint32_t w, uint32_t h, uint32_t tile_w, uint32_t tile_h,
+                     uint32_t frame_count, uint32_t total_frame_index,
+                     uint32_t count, const uint32_t* pixel_xy, const uint32_t* sample_offset,
+                     float* out_rgbjj, rt_stats* stats);
+
+/* Parity entry: intersect_scene (closest hit, occlusion = 0) or
+ * intersect_shadow_ray (occlusion = 1) for `count` rays (RT/intersection.cpp:600-610). */
+int rt_debug_intersect(rt_scene* scene, uint32_t count, const rt_ray_query* rays,
+                       int occlusion, rt_hit_record* out);
+
+/* Record per-stage HIP-event timings into rt_stats::kernel_ms (off by default). */
+int rt_set_profiling(int enable);
+
+/* Size of the in-flight path pool (paths resident in HBM); 0 = default (2^21). */
+int rt_set_path_pool(uint32_t paths);
+
+/* discard_current_render (RT/raytracer.cpp:686-690): polled between wavefront
+ * iterations; the render in flight returns RT_ERROR_CANCELLED. */
+int rt_cancel(rt_scene* scene);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_ABI_H */
