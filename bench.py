@@ -1,0 +1,248 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s (+ samples/s/GPU) of the MI355X wavefront path tracer.
+
+BASELINE.json metric: "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU
+scaling".  The default workload is configs[2] (C3: Cornell box + ~70k-tri
+synthetic mesh with SAH BVH + synthetic 2048x1024 HDR environment + NEE + RR,
+1920x1080, 256 spp, max depth 12) — the 1-GPU configuration the metric is
+quoted on.  One step = one full frame of that workload: every tile of this
+rank's shard (tile t on rank t % N) integrated at 256 spp into an fp32 float4
+accumulation buffer already resident in HBM, plus (N > 1) the RCCL sum-reduce
+of the framebuffer over xGMI.  Strong scaling: the frame is fixed, the tiles
+are split over the ranks.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (k_extend,
+the closest-hit traversal): algorithmic bytes = 48 B per traced ray (read ray
+32 B + write hit 16 B) x rays per launch / mean launch time,
+measured with HIP events on the render stream.  `cpu_baseline` is the CPU
+restatement (oracle/, reference-stream RNG, 64x64 tile queue) timed on this
+box's cores over a bounded sample of the same workload.
+"""
+import argparse
+import ctypes as C
+import importlib.util
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+METRIC = "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table
+EXTEND_BYTES_PER_RAY = 48
+CONFIGS = {
+    "c1": dict(preset="c1", w=512, h=512),
+    "c2": dict(preset="c2", w=1920, h=1080),
+    "c3": dict(preset="c3", w=1920, h=1080),
+    "c4": dict(preset="c4", w=1920, h=1080),
+    "c5": dict(preset="c5", w=3840, h=2160),
+}
+
+
+def import_package():
+    name = "buas_pathtracer_amd"
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(
+        name, os.path.join(ROOT, "buas-pathtracer_amd", "__init__.py"),
+        submodule_search_locations=[os.path.join(ROOT, "buas-pathtracer_amd")])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def cpu_baseline(rt, cfg, spp_override, seconds_budget=15.0):
+    """Oracle (C restatement, reference-stream RNG, tile queue) on a bounded tile sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle_binding as ob
+    lib = ob.load()
+    threads = int(os.environ.get("RT_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    scene, cam, st, fc, post = rt.load_preset(cfg["preset"], cfg["w"], cfg["h"], asset_dir=None)
+    if spp_override:
+        st.samples_per_pixel = spp_override
+    w, h = cfg["w"], cfg["h"]
+    tcx, tcy = (w + 63) // 64, (h + 63) // 64
+    total_tiles = tcx * tcy
+    # calibrate with one tile at the full spp, then size the sample to the budget
+    accum = np.zeros((h, w, 4), np.float32)
+    buf = rt.abi.AccumulationBuffer(w, h, 0, accum.ctypes.data_as(C.POINTER(C.c_float)))
+    desc = scene.desc()
+
+    def run(tiles, nthreads):
+        arr = (C.c_uint32 * len(tiles))(*tiles)
+        stats = rt.abi.Stats()
+        t0 = time.perf_counter()
+        err = lib.oracle_render_tiles(C.byref(desc), C.byref(cam), C.byref(st), C.byref(fc), 64, 64, 0,
+                                      1, nthreads, len(tiles), arr, C.byref(buf), C.byref(stats))
+        assert err == 0
+        return time.perf_counter() - t0, stats
+
+    mid = [total_tiles // 2 + tcx // 2]
+    t1, _ = run(mid, 1)
+    n_tiles = max(threads, min(total_tiles, int(seconds_budget * threads / max(t1, 1e-3))))
+    n_tiles = max(1, (n_tiles // threads) * threads) if n_tiles >= threads else n_tiles
+    step = max(1, total_tiles // n_tiles)
+    tiles = [(k * step + step // 2) % total_tiles for k in range(n_tiles)]
+    dt, stats = run(tiles, threads)
+    rays = stats.closest_hit_rays + stats.shadow_rays
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "samples_per_s": stats.samples / dt,
+            "sample": f"{n_tiles} of {total_tiles} 64x64 tiles (evenly spaced) of the same {w}x{h} "
+                      f"{st.samples_per_pixel}spp frame, reference-stream RNG, {threads} threads, "
+                      f"{dt:.1f} s, {rays} rays"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--spp", type=int, default=0, help="override samples per pixel (0 = config's)")
+    ap.add_argument("--width", type=int, default=0)
+    ap.add_argument("--height", type=int, default=0)
+    ap.add_argument("--pool", type=int, default=0, help="in-flight path pool size (0 = default)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    device = local_rank
+    torch.cuda.set_device(device)
+
+    rt = import_package()
+    cfg = dict(CONFIGS[args.config])
+    if args.width:
+        cfg["w"] = args.width
+    if args.height:
+        cfg["h"] = args.height
+    w, h = cfg["w"], cfg["h"]
+    asset_dir = os.path.join(ROOT, "gpurun_out", "assets") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
+    if asset_dir:
+        os.makedirs(asset_dir, exist_ok=True)
+    scene, cam, st, fc, post = rt.load_preset(cfg["preset"], w, h, asset_dir=asset_dir)
+    if args.spp:
+        st.samples_per_pixel = args.spp
+    if args.pool:
+        rt.lib().rt_set_path_pool(args.pool)
+    dev = rt.DeviceScene(scene, device)
+    accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{device}")
+    stream = torch.cuda.current_stream(device)
+
+    def step():
+        accum.zero_()
+        stats = dev.render_device(cam, st, fc, w, h, accum.data_ptr(), stream=stream.cuda_stream,
+                                  shard_index=rank, shard_count=world)
+        if distributed:
+            dist.reduce(accum, dst=0)          # RCCL sum-reduce of the framebuffer over xGMI
+        return stats
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(device)
+
+    rt.lib().rt_set_profiling(1)
+    closest = shadow = samples = 0
+    kms = [0.0] * 6
+    kl = [0] * 6
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        s = step()
+        closest += s.closest_hit_rays
+        shadow += s.shadow_rays
+        samples += s.samples
+        for k in range(6):
+            kms[k] += s.kernel_ms[k]
+            kl[k] += s.kernel_launches[k]
+    torch.cuda.synchronize(device)
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    rt.lib().rt_set_profiling(0)
+
+    totals = torch.tensor([closest, shadow, samples], dtype=torch.float64, device=f"cuda:{device}")
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+    ext = torch.tensor([kms[1], kl[1], closest], dtype=torch.float64, device=f"cuda:{device}")
+    if distributed:
+        dist.all_reduce(totals, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        ext_r0 = ext.clone()
+    closest_all, shadow_all, samples_all = [float(x) for x in totals.tolist()]
+    elapsed = float(tmax.item())
+
+    if rank == 0:
+        rays = closest_all + shadow_all
+        mrays = rays / elapsed / 1e6
+        # roofline of k_extend on rank 0's stream
+        ext_ms, ext_launches, ext_rays = [float(x) for x in ext.tolist()]
+        mean_launch_s = (ext_ms / 1e3) / max(ext_launches, 1.0)
+        rays_per_launch = ext_rays / max(ext_launches, 1.0)
+        achieved = EXTEND_BYTES_PER_RAY * rays_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("config") == args.config and tj.get("kernel") == "k_extend":
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(rt, cfg, args.spp, args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": round(mrays, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "samples_per_s": round(samples_all / elapsed, 1),
+            "samples_per_s_per_gpu": round(samples_all / elapsed / world, 1),
+            "closest_hit_rays": int(closest_all),
+            "shadow_rays": int(shadow_all),
+            "config": {"workload": f"{args.config}: {cfg['preset']} {w}x{h} {st.samples_per_pixel}spp "
+                                   f"depth {st.max_bounce_count}", "width": w, "height": h,
+                       "spp": st.samples_per_pixel, "max_depth": st.max_bounce_count,
+                       "parallelism": f"tiles%{world}" + ("+rccl_reduce" if world > 1 else "")},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
+                         "kernel": "k_extend", "bytes_per_ray": EXTEND_BYTES_PER_RAY,
+                         "mean_launch_ms": round(mean_launch_s * 1e3, 4),
+                         "rays_per_launch": round(rays_per_launch, 1)},
+            "stage_ms_per_step": {n: round(kms[i] / args.steps, 2) for i, n in
+                                  enumerate(["generate", "extend", "shade", "connect", "splat"])},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    dev.close()
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

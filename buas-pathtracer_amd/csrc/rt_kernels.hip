@@ -415,11 +415,12 @@ RT_D float sample_1d(const DevScene& sc, const SamplerState& s, Rng& rng, int di
 // ======================================================================
 RT_D V3 random_in_unit_sphere(Rng& e) {                                   // :11-19
     V3 r;
+    int guard = 0;   // bounded (a degenerate all-zero RandomSeries would spin forever)
     do {
         float a, b, c, d;
         unilaterals(e, a, b, c, d);
         r = {a*2.0f - 1.0f, b*2.0f - 1.0f, c*2.0f - 1.0f};
-    } while (length_sq(r) >= 1.0f);
+    } while (length_sq(r) >= 1.0f && ++guard < 4096);
     return r;
 }
 RT_D V3 oriented_around_normal(V3 v, V3 n) {                             // :58-75
@@ -638,6 +639,7 @@ RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return b
 // Kernels
 // ======================================================================
 constexpr int BLOCK = 256;
+constexpr int EV_SLOTS = 4;     // iterations between host syncs in run_frame
 
 // k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
 __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
@@ -1033,7 +1035,7 @@ struct rt_scene {
     float* d_lut = nullptr;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
-    hipEvent_t ev[2 * RT_KERNEL_COUNT] = {};
+    hipEvent_t ev[EV_SLOTS * 2 * RT_KERNEL_COUNT] = {};
     bool events = false;
 };
 
@@ -1143,34 +1145,45 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         for (auto& e : s->ev) HIP_OK(hipEventCreate(&e));
         s->events = true;
     }
-    auto stage_begin = [&](int k) { if (prof) (void)hipEventRecord(s->ev[2*k], stream); };
-    auto stage_end = [&](int k) {
-        if (!prof) return;
-        (void)hipEventRecord(s->ev[2*k + 1], stream);
-        (void)hipEventSynchronize(s->ev[2*k + 1]);
-        float ms = 0.0f;
-        (void)hipEventElapsedTime(&ms, s->ev[2*k], s->ev[2*k + 1]);
-        kms[k] += ms; klaunch[k] += 1;
+    // Stage timing without extra host syncs: each iteration records begin/end
+    // events into one of EV_SLOTS ring slots; the slots are read back at the
+    // host sync points the loop already has (every 4 iterations).
+    int pending[EV_SLOTS];
+    int npending = 0;
+    auto ev = [&](int slot, int k, int end) -> hipEvent_t& { return s->ev[(slot*RT_KERNEL_COUNT + k)*2 + end]; };
+    auto stage_begin = [&](int slot, int k) { if (prof) (void)hipEventRecord(ev(slot, k, 0), stream); };
+    auto stage_end = [&](int slot, int k) { if (prof) (void)hipEventRecord(ev(slot, k, 1), stream); };
+    auto harvest = [&]() {
+        for (int i = 0; i < npending; ++i)
+            for (int k = 0; k < RT_KERNEL_COUNT - 1; ++k) {
+                float ms = 0.0f;
+                if (hipEventElapsedTime(&ms, ev(pending[i], k, 0), ev(pending[i], k, 1)) == hipSuccess) {
+                    kms[k] += ms; klaunch[k] += 1;
+                }
+            }
+        npending = 0;
     };
     s->cancel = 0;
     uint64_t iters = 0;
     int cur = 0;
     for (;;) {
-        stage_begin(RT_KERNEL_GENERATE);
+        const int slot = (int)(iters % EV_SLOTS);
+        if (prof) pending[npending++] = slot;
+        stage_begin(slot, RT_KERNEL_GENERATE);
         k_generate<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
-        stage_end(RT_KERNEL_GENERATE);
-        stage_begin(RT_KERNEL_EXTEND);
+        stage_end(slot, RT_KERNEL_GENERATE);
+        stage_begin(slot, RT_KERNEL_EXTEND);
         k_extend<<<grid, BLOCK, 0, stream>>>(s->ds, pool, s->cnt, cur);
-        stage_end(RT_KERNEL_EXTEND);
-        stage_begin(RT_KERNEL_SHADE);
+        stage_end(slot, RT_KERNEL_EXTEND);
+        stage_begin(slot, RT_KERNEL_SHADE);
         k_shade<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
-        stage_end(RT_KERNEL_SHADE);
-        stage_begin(RT_KERNEL_CONNECT);
+        stage_end(slot, RT_KERNEL_SHADE);
+        stage_begin(slot, RT_KERNEL_CONNECT);
         k_connect<<<grid, BLOCK, 0, stream>>>(s->ds, pool, s->cnt);
-        stage_end(RT_KERNEL_CONNECT);
-        stage_begin(RT_KERNEL_SPLAT);
+        stage_end(slot, RT_KERNEL_CONNECT);
+        stage_begin(slot, RT_KERNEL_SPLAT);
         k_splat<<<grid, BLOCK, 0, stream>>>(fp, pool, s->cnt);
-        stage_end(RT_KERNEL_SPLAT);
+        stage_end(slot, RT_KERNEL_SPLAT);
         k_bookkeep<<<1, 64, 0, stream>>>(s->cnt, cur);
         HIP_OK(hipGetLastError());
         ++iters;
@@ -1178,6 +1191,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if ((iters & 3u) == 0u || iters < 4) {
             HIP_OK(hipMemcpyAsync(s->cnt_host, s->cnt, sizeof(Counters), hipMemcpyDeviceToHost, stream));
             HIP_OK(hipStreamSynchronize(stream));
+            harvest();
             const Counters& c = *s->cnt_host;
             if (c.next_sample >= c.total_samples && c.ext_count[cur] == 0) break;
             if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
@@ -1186,6 +1200,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     }
     HIP_OK(hipMemcpyAsync(s->cnt_host, s->cnt, sizeof(Counters), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
+    harvest();
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->closest_hit_rays = s->cnt_host->closest_rays;

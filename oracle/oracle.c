@@ -667,7 +667,8 @@ typedef struct {
 
 static V3 random_in_unit_sphere(RandomSeries* e) {            /* :11-19 */
     V3 r; float u[4];
-    do { random_bilaterals(e, u); r = v3(u[0], u[1], u[2]); } while (length_sq(r) >= 1.0f);
+    int guard = 0;   /* same bound as the device (an all-zero RandomSeries never terminates) */
+    do { random_bilaterals(e, u); r = v3(u[0], u[1], u[2]); } while (length_sq(r) >= 1.0f && ++guard < 4096);
     return r;
 }
 
