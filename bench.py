@@ -235,7 +235,7 @@ def main():
                          "mean_launch_ms": round(mean_launch_s * 1e3, 4),
                          "rays_per_launch": round(rays_per_launch, 1)},
             "stage_ms_per_step": {n: round(kms[i] / args.steps, 2) for i, n in
-                                  enumerate(["generate", "extend", "shade", "connect", "splat"])},
+                                  enumerate(["generate", "extend", "shade", "connect", "splat", "resolve"])},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -29,7 +29,7 @@ RT_HIT_MISS = 0xFFFFFFFF
 RT_HIT_PLANE_BIT = 0x80000000
 RTH_BVH_MIDPOINT_SPLIT, RTH_BVH_SAH_BINNED, RTH_BVH_SAH_FULL = range(3)
 
-RT_KERNEL_NAMES = ("generate", "extend", "shade", "connect", "splat", "reserved")
+RT_KERNEL_NAMES = ("generate", "extend", "shade", "connect", "splat", "resolve")
 RT_KERNEL_COUNT = 6
 
 
@@ -128,8 +128,8 @@ class Stats(C.Structure):
     def as_dict(self):
         return {"closest_hit_rays": self.closest_hit_rays, "shadow_rays": self.shadow_rays,
                 "samples": self.samples, "iterations": self.iterations, "seconds": self.seconds,
-                "kernel_ms": {RT_KERNEL_NAMES[i]: self.kernel_ms[i] for i in range(5)},
-                "kernel_launches": {RT_KERNEL_NAMES[i]: self.kernel_launches[i] for i in range(5)}}
+                "kernel_ms": {RT_KERNEL_NAMES[i]: self.kernel_ms[i] for i in range(6)},
+                "kernel_launches": {RT_KERNEL_NAMES[i]: self.kernel_launches[i] for i in range(6)}}
 
 
 class RayQuery(C.Structure):

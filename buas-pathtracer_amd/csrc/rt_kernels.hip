@@ -525,7 +525,7 @@ struct Pool {
     float4* ray_d;       // d.xyz | w: sample offset bits
     float4* thr;         // throughput.xyz | w: vignette
     float4* L;           // total_color.xyz | w: flags bits (bounce 0-7, specular 8, stack_at 9-15)
-    float4* prev_n;      // prev_N.xyz | w: unused
+    float4* prev_n;      // prev_N.xyz | w: tile-list pixel index p (sample record = s*P + p)
     float2* jitter;
     uint4*  rng;
     float4* hit;         // t | code | tri | v
@@ -572,6 +572,11 @@ struct FrameParams {
     const float* lut;               // 512 floats
     int32_t kernel_size, cache_size;
     float4* accum;
+    // deterministic splat: per-sample records, gathered by k_resolve
+    float4* samp_rgbx;              // [spp*P]: r, g, b, jitter_x   (record = s*P + p)
+    float*  samp_jy;                // [spp*P]: jitter_y
+    const int32_t* tile_base;       // [tiles]: first tile-list pixel of an owned tile, -1 otherwise
+    uint32_t spp;
 };
 
 // wave-aggregated queue append: one atomic per wavefront
@@ -652,12 +657,12 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
     if (active) {
         slot = pool.free_q[cnt->free_count - 1u - i];
         unsigned long long k = cnt->next_sample + i;
-        uint32_t x, y, s;
+        uint32_t x, y, s, p = 0;
         if (fp.list_xy) {
             x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
         } else {
             uint32_t pass = (uint32_t)(k / fp.pixels);
-            uint32_t p = (uint32_t)(k % fp.pixels);
+            p = (uint32_t)(k % fp.pixels);
             uint32_t lo = 0, hi = fp.ntiles;                 // tile_prefix[lo] <= p < tile_prefix[lo+1]
             while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (fp.tile_prefix[mid] <= p) lo = mid; else hi = mid; }
             uint32_t tile = fp.tile_ids[lo];
@@ -697,7 +702,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
         pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
         pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(pack_flags(0, 1, 0)));
-        pool.prev_n[slot] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        pool.prev_n[slot] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(p));
         pool.jitter[slot] = make_float2(jx, jy);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         pool.mstack[slot] = (uint16_t)sc.air_id;            // material_stack[0] = &air
@@ -892,7 +897,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, d4.w);
         pool.thr[slot] = make_float4(thr.x, thr.y, thr.z, t4.w);
         pool.L[slot] = make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at)));
-        pool.prev_n[slot] = make_float4(prev_N.x, prev_N.y, prev_N.z, 0.0f);
+        pool.prev_n[slot] = make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
     }
     const int nxt = cur ^ 1;
@@ -942,6 +947,11 @@ __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Coun
             const uint32_t k = __float_as_uint(pool.ray_d[slot].w);
             float* o = fp.list_out + 5*(size_t)k;
             o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = j.x; o[4] = j.y;
+        } else if (fp.samp_rgbx) {
+            // deterministic path: store the sample; k_resolve gathers it in reference order
+            const size_t rec = (size_t)__float_as_uint(pool.ray_d[slot].w)*fp.pixels + __float_as_uint(pool.prev_n[slot].w);
+            fp.samp_rgbx[rec] = make_float4(r.x, r.y, r.z, j.x);
+            fp.samp_jy[rec] = j.y;
         } else if (fp.cache_size) {
             const int64_t x = pixel % fp.w, y = pixel / fp.w;
             const int64_t ks = fp.kernel_size;
@@ -976,6 +986,67 @@ __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Coun
     // free the slot: positions after the ones generate consumed this iteration
     uint32_t pos = wave_append(&cnt->freed, valid);
     if (valid) pool.free_q[cnt->free_count - n_new_paths(cnt) + pos] = slot;
+}
+
+// k_resolve — splat_filter as a gather (RT/raytracer.cpp:187-259, :476-488).
+// Every output pixel sums its neighbours' samples in exactly the order the
+// reference's single-threaded renderer splats them: tiles in descending index
+// (try_render_next_tile, :555), pixels in raster order inside a tile, samples
+// in order (render_tile, :409-422).  The float additions are therefore the
+// reference's, bit for bit, and need no atomics.
+constexpr int RES_TILE = 16;
+__global__ void __launch_bounds__(RES_TILE*RES_TILE) k_resolve(FrameParams fp) {
+    __shared__ float lut[512];
+    for (int i = threadIdx.x; i < 512; i += RES_TILE*RES_TILE) lut[i] = fp.cache_size ? fp.lut[i] : 0.0f;
+    __syncthreads();
+    const int X = blockIdx.x*RES_TILE + (threadIdx.x % RES_TILE);
+    const int Y = blockIdx.y*RES_TILE + (threadIdx.x / RES_TILE);
+    const int W = (int)fp.w, H = (int)fp.h;
+    if (X >= W || Y >= H) return;
+    const int ks = fp.cache_size ? fp.kernel_size : 0;
+    const float kscale = ks ? (float)(fp.cache_size - 1) / (float)ks : 0.0f;
+    const int TW = (int)fp.tile_w, TH = (int)fp.tile_h;
+    const int x0 = max(X - ks, 0), x1 = min(X + ks, W - 1);
+    const int y0 = max(Y - ks, 0), y1 = min(Y + ks, H - 1);
+    float4 acc = fp.accum[(size_t)Y*W + X];
+    const size_t P = fp.pixels;
+    for (int ty = y1 / TH; ty >= y0 / TH; --ty) {
+        for (int tx = x1 / TW; tx >= x0 / TW; --tx) {
+            const int tile = ty*(int)fp.tcx + tx;
+            const int base = fp.tile_base[tile];
+            if (base < 0) continue;
+            const int min_x = tx*TW, min_y = ty*TH;
+            const int twid = min(W, min_x + TW) - min_x;
+            const int ya = max(y0, min_y), yb = min(y1, min_y + TH - 1);
+            const int xa = max(x0, min_x), xb = min(x1, min_x + TW - 1);
+            for (int y = ya; y <= yb; ++y) {
+                for (int x = xa; x <= xb; ++x) {
+                    const size_t p = (size_t)base + (size_t)(y - min_y)*twid + (size_t)(x - min_x);
+                    if (ks) {
+                        const float dx = (float)(X - x), dy = (float)(Y - y);
+                        for (uint32_t s = 0; s < fp.spp; ++s) {
+                            const size_t r = (size_t)s*P + p;
+                            const float4 c = fp.samp_rgbx[r];
+                            const float jy = fp.samp_jy[r];
+                            const float fx = lut[(int)fabsf(0.5f + kscale*(dx - c.w))];
+                            const float fy = lut[(int)fabsf(0.5f + kscale*(dy - jy))];
+                            const float f = fx*fy;
+                            acc.x = acc.x + f*c.x;
+                            acc.y = acc.y + f*c.y;
+                            acc.z = acc.z + f*c.z;
+                            acc.w = acc.w + f;
+                        }
+                    } else {                                   // box filter: column += (result, 1)
+                        for (uint32_t s = 0; s < fp.spp; ++s) {
+                            const float4 c = fp.samp_rgbx[(size_t)s*P + p];
+                            acc.x = acc.x + c.x; acc.y = acc.y + c.y; acc.z = acc.z + c.z; acc.w = acc.w + 1.0f;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    fp.accum[(size_t)Y*W + X] = acc;
 }
 
 // k_bookkeep — end of iteration: counters roll over (single thread)
@@ -1032,6 +1103,11 @@ struct rt_scene {
     Counters* cnt_host = nullptr;       // pinned
     uint32_t* d_tiles = nullptr;
     size_t tiles_cap = 0;
+    int32_t* d_tile_base = nullptr;
+    size_t tile_base_cap = 0;
+    float4* d_samp = nullptr;       // per-sample records for the deterministic splat
+    float* d_samp_jy = nullptr;
+    size_t samp_cap = 0;
     float* d_lut = nullptr;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
@@ -1366,6 +1442,9 @@ int rt_scene_free(rt_scene* s) {
     if (s->cnt) (void)hipFree(s->cnt);
     if (s->cnt_host) (void)hipHostFree(s->cnt_host);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
+    if (s->d_tile_base) (void)hipFree(s->d_tile_base);
+    if (s->d_samp) (void)hipFree(s->d_samp);
+    if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
     if (s->d_lut) (void)hipFree(s->d_lut);
     if (s->events) for (auto& e : s->ev) (void)hipEventDestroy(e);
     delete s;
@@ -1423,7 +1502,58 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.accum = reinterpret_cast<float4*>(d_pixels);
     unsigned long long total = (unsigned long long)fp.pixels*st->samples_per_pixel;
     if (total == 0) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
-    return run_frame(s, st, fp, total, stream, stats);
+    // Deterministic splat (k_resolve) needs spp*P 20-byte sample records in HBM;
+    // above the budget the frame falls back to float-atomic splats.
+    const char* bud = getenv("RT_SAMPLE_BUDGET_GB");
+    const double budget = (bud ? atof(bud) : 96.0)*1e9;
+    const bool gather = (double)total*20.0 <= budget;
+    if (gather) {
+        if (s->samp_cap < total) {
+            if (s->d_samp) (void)hipFree(s->d_samp);
+            if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
+            s->d_samp = nullptr; s->d_samp_jy = nullptr; s->samp_cap = 0;
+            HIP_OK(hipMalloc(&s->d_samp, sizeof(float4)*total));
+            HIP_OK(hipMalloc(&s->d_samp_jy, sizeof(float)*total));
+            s->samp_cap = total;
+        }
+        const size_t ntile_all = (size_t)fp.tcx*tcy;
+        std::vector<int32_t> base(ntile_all, -1);
+        for (size_t i = 0; i < ids.size(); ++i) base[ids[i]] = (int32_t)prefix[i];
+        if (s->tile_base_cap < ntile_all) {
+            if (s->d_tile_base) (void)hipFree(s->d_tile_base);
+            s->d_tile_base = nullptr;
+            HIP_OK(hipMalloc(&s->d_tile_base, sizeof(int32_t)*ntile_all));
+            s->tile_base_cap = ntile_all;
+        }
+        HIP_OK(hipMemcpyAsync(s->d_tile_base, base.data(), sizeof(int32_t)*ntile_all, hipMemcpyHostToDevice, stream));
+        HIP_OK(hipStreamSynchronize(stream));     // `base` is a host temporary
+        fp.samp_rgbx = s->d_samp;
+        fp.samp_jy = s->d_samp_jy;
+        fp.tile_base = s->d_tile_base;
+        fp.spp = st->samples_per_pixel;
+    }
+    err = run_frame(s, st, fp, total, stream, stats);
+    if (err || !gather) return err;
+    auto t0 = std::chrono::steady_clock::now();
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_profiling) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
+    dim3 rgrid((w + RES_TILE - 1) / RES_TILE, (h + RES_TILE - 1) / RES_TILE);
+    k_resolve<<<rgrid, RES_TILE*RES_TILE, 0, stream>>>(fp);
+    HIP_OK(hipGetLastError());
+    if (g_profiling) HIP_OK(hipEventRecord(e1, stream));
+    HIP_OK(hipStreamSynchronize(stream));
+    if (stats) {
+        stats->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (g_profiling) {
+            float ms = 0.0f;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            stats->kernel_ms[RT_KERNEL_RESOLVE] += ms;
+            stats->kernel_launches[RT_KERNEL_RESOLVE] += 1;
+        }
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return RT_OK;
 }
 
 int rt_render(rt_scene* s, const rt_camera* camera, const rt_settings* st, const rt_filter_cache* filter,

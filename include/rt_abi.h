@@ -192,7 +192,8 @@ enum rt_kernel_id {                 /* wavefront stages, for rt_stats::kernel_ms
     RT_KERNEL_EXTEND   = 1,         /* closest hit (intersect_scene)                     */
     RT_KERNEL_SHADE    = 2,         /* one bounce of advanced_integrator                 */
     RT_KERNEL_CONNECT  = 3,         /* shadow rays (intersect_shadow_ray)                */
-    RT_KERNEL_SPLAT    = 4,         /* splat_filter into the accumulation buffer         */
+    RT_KERNEL_SPLAT    = 4,         /* finished samples -> records (or atomic splat)     */
+    RT_KERNEL_RESOLVE  = 5,         /* splat_filter as a gather in reference order       */
     RT_KERNEL_COUNT    = 6,
 };
 
