@@ -71,13 +71,14 @@ struct DevScene {
     const uint8_t* bluenoise;       // sobol | scrambling | ranking
 };
 
-struct Ray { V3 o, d, inv_d; uint32_t neg; float max_t; };
+struct Ray { V3 o, d, inv_d; uint32_t neg; float max_t; uint32_t zero; };   // zero: axes with d == 0
 
 RT_D Ray make_ray(V3 o, V3 d, float far_clip) {              // RT/intersection.h:13-24
     Ray r;
     r.o = o; r.d = d;
     r.inv_d = sdiv(1.0f, d);
     r.neg = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+    r.zero = (d.x == 0.0f ? 1u : 0u) | (d.y == 0.0f ? 2u : 0u) | (d.z == 0.0f ? 4u : 0u);
     r.max_t = far_clip;
     return r;
 }
@@ -122,6 +123,22 @@ RT_D bool ray_box(const Ray& ray, V3 br, float& t) {               // :76-105
 }
 // ray_intersect_bounding_volume (:107-133) split into the ray/box part (static)
 // and the far-clip test against the current t, done when the node is popped.
+//
+// Degenerate-axis pruning (a performance change that leaves results intact):
+// when a ray component is exactly 0, inv_d is +-inf and the reference's slab
+// test yields NaN on that axis, which the ternary max/min then drop, so the
+// axis is never tested and such a ray visits every node whose other slabs it
+// crosses (~40k nodes of a 70k-triangle mesh for a ray grazing the floor: a
+// 40 ms single-lane tail per launch).  Such a ray keeps that coordinate
+// constant, so a node whose slab on that axis excludes the origin (by more
+// than 1 % of the node's largest half extent, far above the barycentric
+// round-off of the triangle test) contains nothing it can hit: it is skipped.
+// Nodes that are kept get the reference's tn, so visit order, far-clip
+// culling and tie-breaking are unchanged.  Applied inside mesh BVHs only:
+// their leaves hold triangles, whose test is exact for such rays, while the
+// top level holds box primitives whose ray_intersect_box (:76-105) has the
+// same NaN quirk and reports hits the reference keeps (tests/test_gpu_parity.py
+// checks axis-parallel rays against the unpruned oracle).
 RT_D bool bv_static(const Ray& ray, V3 p, V3 r, float& tn_out) {
     V3 rel = sub(ray.o, p);
     V3 m = ray.inv_d;
@@ -132,7 +149,16 @@ RT_D bool bv_static(const Ray& ray, V3 p, V3 r, float& tn_out) {
     float tn = mx(mx(t1.x, t1.y), t1.z);
     float tf = mn(mn(t2.x, t2.y), t2.z);
     tn_out = tn;
-    return (tn < tf) && (tf > 0.0f);
+    bool hit = (tn < tf) && (tf > 0.0f);
+    if (hit && ray.zero) {
+        // margin: 1 % of the node's largest half extent (a triangle's barycentric error is
+        // relative to its own size, which the box bounds) plus 1e-5 of its position
+        const float margin = 0.01f*mx(r.x, mx(r.y, r.z)) + 1e-5f*mx(fabsf(p.x), mx(fabsf(p.y), fabsf(p.z)));
+        if ((ray.zero & 1u) && fabsf(rel.x) > r.x + margin) hit = false;
+        if ((ray.zero & 2u) && fabsf(rel.y) > r.y + margin) hit = false;
+        if ((ray.zero & 4u) && fabsf(rel.z) > r.z + margin) hit = false;
+    }
+    return hit;
 }
 RT_D bool ray_triangle(const Ray& ray, V3 a, V3 e1, V3 e2, float& t, float& ov, float& ow) {   // :135-182
     const float eps = 0.000000001f;
@@ -172,7 +198,28 @@ RT_D void load_child_boxes(const rt_bvh_node* nodes, uint32_t left, V3& p0, V3& 
     p1 = {c.x, c.y, c.z}; r1 = {c.w, d.x, d.y};
 }
 
-constexpr int STACK_DEPTH = 64;     // the reference's node_stack[64] (RT/intersection.cpp:261, :445)
+// ----------------------------------------------------------------------
+// Scene traversal as a step machine.
+//
+// intersect_scene_internal (RT/intersection.cpp:411-598) restated as a
+// sequence of small steps (one node, one leaf primitive or one mesh leaf per
+// step) so that a persistent wave can refill lanes whose ray has finished
+// instead of idling until the slowest lane's nested mesh traversal ends.
+// The visit order is exactly the reference's: planes first, then the
+// top-level BVH front-to-back by d_is_negative[split_axis]; each leaf's
+// primitives in order, a mesh instance traversed completely (its own BVH,
+// object-space ray) before the leaf's next primitive; far-clip culling of a
+// node against the current t when the node is popped.  Children are box-
+// tested when their parent is expanded and only hits are pushed together
+// with their entry distance tn, which is exactly the reference's pop-time
+// test (ray_intersect_bounding_volume, :107-133) split in two.
+//
+// Stack: per-lane, STACK_LDS entries in LDS ([level][lane], bank-conflict
+// free), deeper levels spill to a per-thread global area.  Total depth 64 =
+// the reference's node_stack[64] (:261, :445).
+// ----------------------------------------------------------------------
+constexpr int STACK_DEPTH = 64;
+constexpr int STACK_LDS = 16;
 
 struct Hit {
     float t;
@@ -181,129 +228,158 @@ struct Hit {
     float v, w;         // barycentrics of that triangle (uvw = (1-v-w, v, w))
 };
 
-// Closest-hit (OCC = false) or any-hit (OCC = true) scene query:
-// intersect_scene_internal (RT/intersection.cpp:411-598) without the normal step.
-// Traversal visits nodes in exactly the reference's order (front-to-back by
-// d_is_negative[split_axis], far-clip culling against the current t at pop time),
-// so ties resolve identically.
+struct Stack {
+    uint2* lds;         // [STACK_LDS][block] for this block
+    uint2* spill;       // [STACK_DEPTH - STACK_LDS][nthreads] global
+    uint32_t lane, block, gtid, nthreads;
+    RT_D void put(int level, uint32_t node, float tn) const {
+        uint2 e = make_uint2(node, __float_as_uint(tn));
+        if (level < STACK_LDS) lds[level*block + lane] = e;
+        else spill[(size_t)(level - STACK_LDS)*nthreads + gtid] = e;
+    }
+    RT_D uint2 get(int level) const {
+        return level < STACK_LDS ? lds[level*block + lane] : spill[(size_t)(level - STACK_LDS)*nthreads + gtid];
+    }
+};
+
+enum { TM_TOP = 0, TM_LEAF = 1, TM_MESH = 2, TM_DONE = 3 };
+
 template <bool OCC>
-__device__ __noinline__ bool intersect(const DevScene& sc, const Ray& ray, uint32_t ignored, Hit& h) {
-    float t = ray.max_t;
-    uint32_t code = RT_HIT_MISS, tri = 0;
-    float hv = 0.0f, hw = 0.0f;
-    for (uint32_t i = 0; i < sc.plane_count; ++i) {
-        const rt_primitive& pl = sc.planes[i];
-        if (ray_plane(ray, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], t)) {
-            code = RT_HIT_PLANE_BIT | i;
-            if (OCC) { h.t = t; h.code = code; return true; }
-        }
-    }
-    uint32_t stk_node[STACK_DEPTH];
-    float stk_tn[STACK_DEPTH];
-    int sp = 0;
-    if (sc.bvh_node_count) {
-        V3 p, r; uint32_t lf, cnt, ax;
-        load_node(sc.bvh, 0, p, r, lf, cnt, ax);
-        float tn;
-        if (bv_static(ray, p, r, tn)) { stk_node[0] = 0; stk_tn[0] = tn; sp = 1; }
-    }
-    while (sp > 0) {
-        --sp;
-        uint32_t ni = stk_node[sp];
-        if (!(stk_tn[sp] < t)) continue;
-        V3 p, r; uint32_t lf, cnt, ax;
-        load_node(sc.bvh, ni, p, r, lf, cnt, ax);
-        if (cnt) {
-            for (uint32_t li = 0; li < cnt; ++li) {
-                uint32_t pi = sc.bvh_idx[lf + li];
-                if (pi == ignored) continue;
-                const rt_primitive prim = sc.prims[pi];
-                const M34 inv = load_m34(&sc.inv[prim.transform_index]);
-                Ray ir = make_ray(xform(inv, ray.o, 1.0f), xform(inv, ray.d, 0.0f), ray.max_t);   // transform_ray :403-409
-                bool hit_any = false;
-                if (prim.type == RT_PRIMITIVE_SPHERE) {
-                    hit_any = ray_sphere(ir, prim.p[0], t);
-                } else if (prim.type == RT_PRIMITIVE_BOX) {
-                    hit_any = ray_box(ir, {prim.p[0], prim.p[1], prim.p[2]}, t);
-                } else if (prim.type == RT_PRIMITIVE_MESH) {       // intersect_mesh :243-401
-                    const DevMesh mesh = sc.meshes[prim.mesh_index];
-                    const rt_bvh_node* mn_ = sc.mnodes + mesh.node_offset;
-                    uint32_t mtri = 0xFFFFFFFFu;
-                    float mv = 0.0f, mw = 0.0f;
-                    int base = sp;
-                    {
-                        V3 rp, rr; uint32_t rlf, rcnt, rax;
-                        load_node(mn_, 0, rp, rr, rlf, rcnt, rax);
-                        float tn;
-                        if (sp < STACK_DEPTH && bv_static(ir, rp, rr, tn)) { stk_node[sp] = 0; stk_tn[sp] = tn; ++sp; }
-                    }
-                    bool occluded = false;
-                    while (sp > base) {
-                        --sp;
-                        uint32_t mi = stk_node[sp];
-                        if (!(stk_tn[sp] < t)) continue;
-                        V3 np, nr; uint32_t nlf, ncnt, nax;
-                        load_node(mn_, mi, np, nr, nlf, ncnt, nax);
-                        if (ncnt) {
-                            const uint32_t g0 = mesh.tri_offset + nlf;
-                            for (uint32_t k = 0; k < ncnt; ++k) {
-                                const float4* tp = sc.tris + 3*(size_t)(g0 + k);
-                                float4 ta = tp[0], tb = tp[1], tc = tp[2];
-                                float v, w;
-                                if (ray_triangle(ir, ld3(ta), ld3(tb), ld3(tc), t, v, w)) {
-                                    if (OCC) { occluded = true; break; }
-                                    mtri = g0 + k; mv = v; mw = w;
-                                }
-                            }
-                            if (OCC && occluded) break;
-                        } else {
-                            V3 p0, r0, p1, r1;
-                            load_child_boxes(mn_, nlf, p0, r0, p1, r1);
-                            float tn0, tn1;
-                            bool h0 = bv_static(ir, p0, r0, tn0);
-                            bool h1 = bv_static(ir, p1, r1, tn1);
-                            // the reference pushes both children; the one pushed second is popped first
-                            bool left_first_pop = !((ir.neg >> nax) & 1u);
-                            if (left_first_pop) {
-                                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = nlf + 1; stk_tn[sp] = tn1; ++sp; }
-                                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = nlf; stk_tn[sp] = tn0; ++sp; }
-                            } else {
-                                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = nlf; stk_tn[sp] = tn0; ++sp; }
-                                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = nlf + 1; stk_tn[sp] = tn1; ++sp; }
-                            }
-                        }
-                    }
-                    if (OCC) {
-                        if (occluded) { h.t = t; h.code = pi; return true; }
-                    } else if (mtri != 0xFFFFFFFFu) {
-                        hit_any = true; tri = mtri; hv = mv; hw = mw;
-                    }
-                    sp = base;
-                }
-                if (hit_any) {
-                    if (OCC) { h.t = t; h.code = pi; return true; }
-                    code = pi;
-                }
-            }
+struct Traversal {
+    Ray wr;             // world ray
+    V3 co, cd, cinv;    // current ray (object space while in a mesh)
+    uint32_t cneg, czero;
+    float t;
+    uint32_t code, tri;
+    float hv, hw;
+    uint32_t ignored;
+    int sp, mode;
+    uint32_t leaf_first, leaf_count, leaf_i;
+    uint32_t inst, node_off, tri_off;
+    int mesh_base;
+    uint32_t mtri;
+    float mv, mw;
+    bool occluded;
+
+    RT_D void push_children(const Stack& st, const rt_bvh_node* nodes, uint32_t lf, uint32_t ax) {
+        V3 p0, r0, p1, r1;
+        load_child_boxes(nodes, lf, p0, r0, p1, r1);
+        Ray r; r.o = co; r.d = cd; r.inv_d = cinv; r.zero = czero;
+        float tn0, tn1;
+        const bool h0 = bv_static(r, p0, r0, tn0);
+        const bool h1 = bv_static(r, p1, r1, tn1);
+        // the reference pushes (left, left+1) or (left+1, left); the second is popped first
+        if (!((cneg >> ax) & 1u)) {
+            if (h1 && sp < STACK_DEPTH) st.put(sp++, lf + 1, tn1);
+            if (h0 && sp < STACK_DEPTH) st.put(sp++, lf, tn0);
         } else {
-            V3 p0, r0, p1, r1;
-            load_child_boxes(sc.bvh, lf, p0, r0, p1, r1);
-            float tn0, tn1;
-            bool h0 = bv_static(ray, p0, r0, tn0);
-            bool h1 = bv_static(ray, p1, r1, tn1);
-            bool left_first_pop = !((ray.neg >> ax) & 1u);
-            if (left_first_pop) {
-                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = lf + 1; stk_tn[sp] = tn1; ++sp; }
-                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = lf; stk_tn[sp] = tn0; ++sp; }
-            } else {
-                if (h0 && sp < STACK_DEPTH) { stk_node[sp] = lf; stk_tn[sp] = tn0; ++sp; }
-                if (h1 && sp < STACK_DEPTH) { stk_node[sp] = lf + 1; stk_tn[sp] = tn1; ++sp; }
-            }
+            if (h0 && sp < STACK_DEPTH) st.put(sp++, lf, tn0);
+            if (h1 && sp < STACK_DEPTH) st.put(sp++, lf + 1, tn1);
         }
     }
-    h.t = t; h.code = code; h.tri = tri; h.v = hv; h.w = hw;
-    return code != RT_HIT_MISS;
-}
+
+    // Pruning stays off for the world ray: the top level holds box primitives, whose own
+    // slab test (ray_intersect_box) inherits the NaN quirk and can report a hit far away.
+    RT_D void set_world() { co = wr.o; cd = wr.d; cinv = wr.inv_d; cneg = wr.neg; czero = 0u; }
+
+    RT_D void init(const DevScene& sc, const Stack& st, V3 o, V3 d, float max_t, uint32_t ign) {
+        wr = make_ray(o, d, max_t);
+        wr.zero = 0u;
+        set_world();
+        t = max_t; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
+        ignored = ign; sp = 0; mode = TM_TOP; occluded = false;
+        for (uint32_t i = 0; i < sc.plane_count; ++i) {            // planes, brute force (:424-433)
+            const rt_primitive& pl = sc.planes[i];
+            if (ray_plane(wr, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], t)) {
+                code = RT_HIT_PLANE_BIT | i;
+                if (OCC) { occluded = true; mode = TM_DONE; return; }
+            }
+        }
+        if (sc.bvh_node_count) {
+            V3 p, r; uint32_t lf, cnt, ax;
+            load_node(sc.bvh, 0, p, r, lf, cnt, ax);
+            float tn;
+            if (bv_static(wr, p, r, tn)) st.put(sp++, 0u, tn);
+        }
+    }
+
+    // One traversal step; returns false once the query is finished (mode == TM_DONE).
+    RT_D bool step(const DevScene& sc, const Stack& st) {
+        if (mode == TM_MESH) {
+            if (sp == mesh_base) {                                 // instance finished
+                if (mtri != 0xFFFFFFFFu) { code = inst; tri = mtri; hv = mv; hw = mw; }
+                mode = TM_LEAF;
+                set_world();
+                return true;
+            }
+            const uint2 e = st.get(--sp);
+            if (!(__uint_as_float(e.y) < t)) return true;
+            const rt_bvh_node* mn_ = sc.mnodes + node_off;
+            V3 np, nr; uint32_t lf, cnt, ax;
+            load_node(mn_, e.x, np, nr, lf, cnt, ax);
+            if (cnt) {
+                Ray r; r.o = co; r.d = cd;
+                const uint32_t g0 = tri_off + lf;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const float4* tp = sc.tris + 3*(size_t)(g0 + k);
+                    const float4 ta = tp[0], tb = tp[1], tc = tp[2];
+                    float v, w;
+                    if (ray_triangle(r, ld3(ta), ld3(tb), ld3(tc), t, v, w)) {
+                        if (OCC) { occluded = true; mode = TM_DONE; return false; }
+                        mtri = g0 + k; mv = v; mw = w;
+                    }
+                }
+            } else {
+                push_children(st, mn_, lf, ax);
+            }
+            return true;
+        }
+        if (mode == TM_LEAF) {
+            if (leaf_i == leaf_count) { mode = TM_TOP; return true; }
+            const uint32_t pi = sc.bvh_idx[leaf_first + leaf_i++];
+            if (pi == ignored) return true;
+            const rt_primitive prim = sc.prims[pi];
+            const M34 inv = load_m34(&sc.inv[prim.transform_index]);
+            Ray ir = make_ray(xform(inv, wr.o, 1.0f), xform(inv, wr.d, 0.0f), wr.max_t);   // transform_ray :403-409
+            if (prim.type == RT_PRIMITIVE_MESH) {                 // intersect_mesh :243-401
+                const DevMesh mesh = sc.meshes[prim.mesh_index];
+                co = ir.o; cd = ir.d; cinv = ir.inv_d; cneg = ir.neg; czero = ir.zero;
+                inst = pi; node_off = mesh.node_offset; tri_off = mesh.tri_offset;
+                mesh_base = sp; mtri = 0xFFFFFFFFu;
+                V3 rp, rr; uint32_t rlf, rcnt, rax;
+                load_node(sc.mnodes + node_off, 0, rp, rr, rlf, rcnt, rax);
+                float tn;
+                if (sp < STACK_DEPTH && bv_static(ir, rp, rr, tn)) st.put(sp++, 0u, tn);
+                mode = TM_MESH;
+                return true;
+            }
+            bool hit = false;
+            if (prim.type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, prim.p[0], t);
+            else if (prim.type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {prim.p[0], prim.p[1], prim.p[2]}, t);
+            if (hit) {
+                if (OCC) { occluded = true; mode = TM_DONE; return false; }
+                code = pi;
+            }
+            return true;
+        }
+        if (mode == TM_TOP) {
+            if (sp == 0) { mode = TM_DONE; return false; }
+            const uint2 e = st.get(--sp);
+            if (!(__uint_as_float(e.y) < t)) return true;
+            V3 p, r; uint32_t lf, cnt, ax;
+            load_node(sc.bvh, e.x, p, r, lf, cnt, ax);
+            if (cnt) { leaf_first = lf; leaf_count = cnt; leaf_i = 0; mode = TM_LEAF; }
+            else push_children(st, sc.bvh, lf, ax);
+            return true;
+        }
+        return false;
+    }
+
+    RT_D Hit result() const {
+        Hit h; h.t = t; h.code = OCC ? (occluded ? 0u : RT_HIT_MISS) : code; h.tri = tri; h.v = hv; h.w = hw;
+        return h;
+    }
+};
 
 // :NormalCalculation (RT/intersection.cpp:526-591)
 RT_D void hit_geometry(const DevScene& sc, const Ray& ray, const Hit& h, V3& I, V3& N, uint32_t& material_id) {
@@ -548,6 +624,9 @@ struct Counters {
     uint32_t freed;
     uint32_t cancel;
     uint32_t pad;
+    uint32_t fetch[2];              // persistent trace kernels: items handed out (extend, connect)
+    uint32_t max_steps[2];          // diagnostics: longest traversal (steps) per kind
+    float    worst_ray[2][8];       // o.xyz, d.xyz, max_t, steps of a ray above the step threshold
     unsigned long long next_sample;
     unsigned long long total_samples;
     unsigned long long closest_rays;
@@ -715,17 +794,90 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
     if (active && !enqueue) pool.done_q[dpos] = slot;
 }
 
-// k_extend — intersect_scene for every queued path (RT/intersection.cpp:606-610)
-__global__ void __launch_bounds__(BLOCK) k_extend(DevScene sc, Pool pool, const Counters* cnt, int cur) {
-    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
-    if (q >= cnt->ext_count[cur]) return;
-    const uint32_t slot = pool.ext_q[cur][q];
-    float4 o = pool.ray_o[slot], d = pool.ray_d[slot];
-    Ray ray = make_ray(ld3(o), ld3(d), FLT_MAX_);
-    Hit h;
-    intersect<false>(sc, ray, 0, h);
-    pool.hit[slot] = make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v);
-    pool.hit_w[slot] = h.w;
+// k_trace<false> — intersect_scene for every queued path (RT/intersection.cpp:606-610)
+// k_trace<true>  — intersect_shadow_ray for every queued shadow ray (:600-604,
+//                  RT/integrators.cpp:756); unoccluded NEE contributions are
+//                  added to the path's total_color.
+// Persistent waves: each wave grabs CHUNK queue items with one atomic and
+// refills lanes whose query has finished from that chunk (Aila & Laine 2009,
+// for 64-wide waves), so lanes do not idle behind the wave's longest ray.
+constexpr int TB = 256;
+constexpr uint32_t CHUNK = 256;
+constexpr int STEPS_PER_REFILL = 8;
+
+template <bool OCC>
+__global__ void __launch_bounds__(TB) k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill) {
+    __shared__ uint2 lds_stack[STACK_LDS*TB];
+    Stack st;
+    st.lds = lds_stack; st.spill = spill; st.lane = threadIdx.x; st.block = TB;
+    st.gtid = blockIdx.x*TB + threadIdx.x; st.nthreads = gridDim.x*TB;
+    const uint32_t count = OCC ? cnt->shadow_count : cnt->ext_count[cur];
+    uint32_t* fetch = &cnt->fetch[OCC ? 1 : 0];
+    const uint32_t lane = __lane_id();
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    uint32_t chunk_next = 0, chunk_end = 0;
+    bool exhausted = false, active = false;
+    uint32_t item = 0;
+    uint32_t steps = 0;
+    Traversal<OCC> tr;
+    auto finish = [&]() {
+        atomicMax(&cnt->max_steps[OCC ? 1 : 0], steps);
+        if (steps > 20000u) {
+            float* w = cnt->worst_ray[OCC ? 1 : 0];
+            w[0] = tr.wr.o.x; w[1] = tr.wr.o.y; w[2] = tr.wr.o.z;
+            w[3] = tr.wr.d.x; w[4] = tr.wr.d.y; w[5] = tr.wr.d.z; w[6] = tr.wr.max_t; w[7] = (float)steps;
+        }
+        if (OCC) {
+            if (!tr.occluded) {
+                const uint32_t slot = pool.sh_slot[item];
+                const float4 c = pool.sh_c[item];
+                float4 L = pool.L[slot];
+                L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;   // total_color += ... (:768)
+                pool.L[slot] = L;
+            }
+        } else {
+            const uint32_t slot = pool.ext_q[cur][item];
+            const Hit h = tr.result();
+            pool.hit[slot] = make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v);
+            pool.hit_w[slot] = h.w;
+        }
+    };
+    for (;;) {
+        unsigned long long idle = __ballot(!active);
+        while (idle && !exhausted) {
+            if (chunk_next >= chunk_end) {
+                uint32_t base = 0;
+                if (lane == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) base = atomicAdd(fetch, CHUNK);
+                base = __shfl(base, __ffsll((long long)__ballot(true)) - 1);
+                if (base >= count) { exhausted = true; break; }
+                chunk_next = base;
+                chunk_end = min(base + CHUNK, count);
+            }
+            const uint32_t avail = chunk_end - chunk_next;
+            const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+            if (!active && rank < avail) {
+                item = chunk_next + rank;
+                if (OCC) {
+                    const float4 o = pool.sh_o[item], d = pool.sh_d[item];
+                    tr.init(sc, st, ld3(o), ld3(d), d.w, __float_as_uint(o.w));
+                } else {
+                    const uint32_t slot = pool.ext_q[cur][item];
+                    tr.init(sc, st, ld3(pool.ray_o[slot]), ld3(pool.ray_d[slot]), FLT_MAX_, 0u);
+                }
+                steps = 0;
+                if (tr.mode == TM_DONE) finish(); else active = true;
+            }
+            chunk_next += min((uint32_t)__popcll(idle), avail);
+            idle = __ballot(!active);
+        }
+        if (__ballot(active) == 0ull) break;
+        if (active) {
+            for (int k = 0; k < STEPS_PER_REFILL; ++k) {
+                ++steps;
+                if (!tr.step(sc, st)) { finish(); active = false; break; }
+            }
+        }
+    }
 }
 
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
@@ -914,22 +1066,6 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
     if (done) pool.done_q[dpos] = slot;
 }
 
-// k_connect — intersect_shadow_ray (RT/integrators.cpp:756, RT/intersection.cpp:600-604)
-__global__ void __launch_bounds__(BLOCK) k_connect(DevScene sc, Pool pool, const Counters* cnt) {
-    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
-    if (q >= cnt->shadow_count) return;
-    const float4 o = pool.sh_o[q], d = pool.sh_d[q];
-    Ray ray = make_ray(ld3(o), ld3(d), d.w);
-    Hit h;
-    if (!intersect<true>(sc, ray, __float_as_uint(o.w), h)) {
-        const uint32_t slot = pool.sh_slot[q];
-        const float4 c = pool.sh_c[q];
-        float4 L = pool.L[slot];
-        L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;
-        pool.L[slot] = L;
-    }
-}
-
 // k_splat — vignette + splat_filter (RT/raytracer.cpp:469-488, 187-259) with
 // float atomics, then the slot returns to the free list.
 __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Counters* cnt) {
@@ -1061,6 +1197,8 @@ __global__ void k_bookkeep(Counters* cnt, int cur) {
     cnt->ext_count[cur] = 0;
     cnt->shadow_count = 0;
     cnt->done_count = 0;
+    cnt->fetch[0] = 0;
+    cnt->fetch[1] = 0;
 }
 
 __global__ void k_init_free(uint32_t* free_q, uint32_t n) {
@@ -1068,19 +1206,28 @@ __global__ void k_init_free(uint32_t* free_q, uint32_t n) {
     if (i < n) free_q[i] = n - 1u - i;       // slot 0 handed out first
 }
 
-// debug / parity kernel: intersect_scene / intersect_shadow_ray for explicit rays
-__global__ void k_debug_intersect(DevScene sc, const rt_ray_query* rays, rt_hit_record* out, uint32_t n, int occ) {
+// debug / parity kernel: intersect_scene / intersect_shadow_ray for explicit rays,
+// through the same Traversal step machine as k_trace (one ray per thread).
+template <bool OCC>
+__global__ void __launch_bounds__(128) k_debug_intersect(DevScene sc, const rt_ray_query* rays, rt_hit_record* out,
+                                                         uint32_t n, uint2* spill) {
+    __shared__ uint2 lds_stack[STACK_LDS*128];
+    Stack st;
+    st.lds = lds_stack; st.spill = spill; st.lane = threadIdx.x; st.block = 128;
+    st.gtid = blockIdx.x*128 + threadIdx.x; st.nthreads = gridDim.x*128;
     uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
     if (i >= n) return;
     rt_ray_query rq = rays[i];
-    Ray ray = make_ray(rv3(rq.o), rv3(rq.d), rq.max_t);
-    Hit h;
+    Traversal<OCC> tr;
+    tr.init(sc, st, rv3(rq.o), rv3(rq.d), rq.max_t, rq.ignored_primitive);
+    while (tr.mode != TM_DONE && tr.step(sc, st)) {}
+    const Hit h = tr.result();
     rt_hit_record r;
     memset(&r, 0, sizeof(r));
-    bool hit = occ ? intersect<true>(sc, ray, rq.ignored_primitive, h) : intersect<false>(sc, ray, rq.ignored_primitive, h);
     r.t = h.t;
-    r.primitive = hit ? h.code : RT_HIT_MISS;
-    if (hit && !occ) {
+    r.primitive = h.code;
+    if (!OCC && h.code != RT_HIT_MISS) {
+        Ray ray = make_ray(rv3(rq.o), rv3(rq.d), rq.max_t);
         V3 I, N; uint32_t mid;
         hit_geometry(sc, ray, h, I, N, mid);
         r.hit_p = {I.x, I.y, I.z};
@@ -1105,6 +1252,8 @@ struct rt_scene {
     size_t tiles_cap = 0;
     int32_t* d_tile_base = nullptr;
     size_t tile_base_cap = 0;
+    uint2* d_spill = nullptr;       // traversal stack levels beyond STACK_LDS
+    uint32_t trace_grid = 0;        // persistent k_trace blocks
     float4* d_samp = nullptr;       // per-sample records for the deterministic splat
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
@@ -1249,13 +1398,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         k_generate<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
         stage_end(slot, RT_KERNEL_GENERATE);
         stage_begin(slot, RT_KERNEL_EXTEND);
-        k_extend<<<grid, BLOCK, 0, stream>>>(s->ds, pool, s->cnt, cur);
+        k_trace<false><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill);
         stage_end(slot, RT_KERNEL_EXTEND);
         stage_begin(slot, RT_KERNEL_SHADE);
         k_shade<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
         stage_end(slot, RT_KERNEL_SHADE);
         stage_begin(slot, RT_KERNEL_CONNECT);
-        k_connect<<<grid, BLOCK, 0, stream>>>(s->ds, pool, s->cnt);
+        k_trace<true><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill);
         stage_end(slot, RT_KERNEL_CONNECT);
         stage_begin(slot, RT_KERNEL_SPLAT);
         k_splat<<<grid, BLOCK, 0, stream>>>(fp, pool, s->cnt);
@@ -1277,6 +1426,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     HIP_OK(hipMemcpyAsync(s->cnt_host, s->cnt, sizeof(Counters), hipMemcpyDeviceToHost, stream));
     HIP_OK(hipStreamSynchronize(stream));
     harvest();
+    if (getenv("RT_DEBUG_TRAVERSAL")) {
+        const Counters& c = *s->cnt_host;
+        for (int k = 0; k < 2; ++k)
+            fprintf(stderr, "[rt] %s: max steps %u; worst ray o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) max_t=%.9g steps=%.0f\n",
+                    k ? "shadow" : "closest", c.max_steps[k], c.worst_ray[k][0], c.worst_ray[k][1], c.worst_ray[k][2],
+                    c.worst_ray[k][3], c.worst_ray[k][4], c.worst_ray[k][5], c.worst_ray[k][6], c.worst_ray[k][7]);
+    }
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->closest_hit_rays = s->cnt_host->closest_rays;
@@ -1427,6 +1583,15 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     ds.bot_sky = rv3(d->bot_sky_color);
     if ((err = upload(s, rt_dev_strata_tab, sizeof(rt_dev_strata_tab), &ds.strata))) return fail(err);
     if ((err = upload(s, rt_dev_bluenoise_tab, sizeof(rt_dev_bluenoise_tab), &ds.bluenoise))) return fail(err);
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("hipGetDeviceProperties"); return fail(RT_ERROR_DEVICE); }
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
+        const size_t spill_bytes = sizeof(uint2)*(size_t)(STACK_DEPTH - STACK_LDS)*s->trace_grid*TB;
+        if (hipMalloc(&s->d_spill, spill_bytes) != hipSuccess) { set_error("hipMalloc spill"); return fail(RT_ERROR_OUT_OF_MEMORY); }
+    }
     if (hipMalloc(&s->cnt, sizeof(Counters)) != hipSuccess) { set_error("hipMalloc counters"); return fail(RT_ERROR_OUT_OF_MEMORY); }
     if (hipHostMalloc(&s->cnt_host, sizeof(Counters)) != hipSuccess) { set_error("hipHostMalloc"); return fail(RT_ERROR_OUT_OF_MEMORY); }
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
@@ -1443,6 +1608,7 @@ int rt_scene_free(rt_scene* s) {
     if (s->cnt_host) (void)hipHostFree(s->cnt_host);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     if (s->d_tile_base) (void)hipFree(s->d_tile_base);
+    if (s->d_spill) (void)hipFree(s->d_spill);
     if (s->d_samp) (void)hipFree(s->d_samp);
     if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
     if (s->d_lut) (void)hipFree(s->d_lut);
@@ -1610,8 +1776,14 @@ int rt_debug_intersect(rt_scene* s, uint32_t count, const rt_ray_query* rays, in
     HIP_OK(hipMalloc(&d_r, sizeof(rt_ray_query)*count));
     HIP_OK(hipMalloc(&d_o, sizeof(rt_hit_record)*count));
     HIP_OK(hipMemcpy(d_r, rays, sizeof(rt_ray_query)*count, hipMemcpyHostToDevice));
-    k_debug_intersect<<<(count + 127) / 128, 128>>>(s->ds, d_r, d_o, count, occlusion);
+    uint2* d_sp = nullptr;
+    const uint32_t dgrid = (count + 127) / 128;
+    HIP_OK(hipMalloc(&d_sp, sizeof(uint2)*(size_t)(STACK_DEPTH - STACK_LDS)*dgrid*128));
+    if (occlusion) k_debug_intersect<true><<<dgrid, 128>>>(s->ds, d_r, d_o, count, d_sp);
+    else k_debug_intersect<false><<<dgrid, 128>>>(s->ds, d_r, d_o, count, d_sp);
     HIP_OK(hipGetLastError());
+    HIP_OK(hipDeviceSynchronize());
+    (void)hipFree(d_sp);
     HIP_OK(hipMemcpy(out, d_o, sizeof(rt_hit_record)*count, hipMemcpyDeviceToHost));
     (void)hipFree(d_r); (void)hipFree(d_o);
     return RT_OK;
