@@ -145,13 +145,16 @@ def main():
     accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{device}")
     stream = torch.cuda.current_stream(device)
 
+    from buas_pathtracer_amd.sharding import render_frame_sharded
+
+    def render_shard(shard_index, shard_count, buf):
+        return dev.render_device(cam, st, fc, w, h, buf.data_ptr(), stream=stream.cuda_stream,
+                                 shard_index=shard_index, shard_count=shard_count)
+
     def step():
         accum.zero_()
-        stats = dev.render_device(cam, st, fc, w, h, accum.data_ptr(), stream=stream.cuda_stream,
-                                  shard_index=rank, shard_count=world)
-        if distributed:
-            dist.reduce(accum, dst=0)          # RCCL sum-reduce of the framebuffer over xGMI
-        return stats
+        # tiles t % world == rank, then the RCCL sum-reduce of the framebuffer over xGMI
+        return render_frame_sharded(render_shard, accum, rank, world)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,50 @@
+"""The C-ABI library loads and exports every function declared in include/*.h;
+without a GPU the product refuses to run (no CPU fallback)."""
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in ("rt_abi.h", "rt_host.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        for m in re.finditer(r"^[A-Za-z_][\w\s\*]*?\b(rth?_\w+)\s*\(", text, flags=re.M):
+            names.add(m.group(1))
+    return sorted(names)
+
+
+def test_every_declared_symbol_is_exported(rt):
+    lib = rt.lib()
+    names = declared_functions()
+    assert len(names) > 40
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    assert lib.rt_abi_version() == 1
+
+
+def test_ctypes_table_covers_header(rt):
+    from buas_pathtracer_amd.abi import ABI_FUNCTIONS, HOST_FUNCTIONS
+    assert set(declared_functions()) == set(ABI_FUNCTIONS) | set(HOST_FUNCTIONS)
+
+
+def test_struct_sizes_match_reference_layout(rt):
+    import ctypes as C
+    a = rt.abi
+    assert C.sizeof(a.Material) == 68                  # RT/scene.h:15-29
+    assert C.sizeof(a.BvhNode) == 32                   # RT/bvh.h:31-37
+    assert C.sizeof(a.M4x4Inv) == 128
+    assert C.sizeof(a.FilterCache) == 8 + 512 * 4     # RT/Raytracer.h:34-40
+
+
+def test_no_cpu_fallback_without_gpu(rt):
+    if rt.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    scene, cam, st, fc, post = rt.load_preset("c1", 32, 32)
+    with pytest.raises(rt.RenderError) as e:
+        rt.DeviceScene(scene, 0)
+    assert e.value.code == rt.abi.RT_ERROR_NO_DEVICE
