@@ -16,6 +16,20 @@ import oracle_binding as ob
 
 pytestmark = pytest.mark.gpu
 
+REPORT = {}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _parity_report():
+    """Write the measured parity figures to gpurun_out/parity_report.json (cited in DESIGN.md)."""
+    yield
+    import json
+    import os
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "parity_report.json"), "w") as f:
+        json.dump(REPORT, f, indent=1)
+
 
 def rel_l2(a, b):
     a = a.astype(np.float64)
@@ -66,6 +80,7 @@ def test_intersect_bit_exact(which, occlusion, request):
         elif a.primitive != b.primitive or (a.primitive != 0xFFFFFFFF and (
                 a.t != b.t or tuple(a.n) != tuple(b.n) or tuple(a.hit_p) != tuple(b.hit_p))):
             mism += 1
+    REPORT[f"intersect_{which}_{'occ' if occlusion else 'closest'}"] = {"rays": len(rays), "mismatches": int(mism)}
     assert mism == 0, f"{mism} of {len(rays)} hit records differ"
 
 
@@ -100,6 +115,8 @@ def test_axis_parallel_rays_bit_exact(occlusion, c3small):
                 a.t != b.t or tuple(a.n) != tuple(b.n) or tuple(a.hit_p) != tuple(b.hit_p))):
             mism += 1
     hits = sum(b.primitive != 0xFFFFFFFF for b in o)
+    REPORT[f"axis_parallel_{'occ' if occlusion else 'closest'}"] = {"rays": len(rays), "hits": int(hits),
+                                                                     "mismatches": int(mism)}
     assert hits > 1000
     assert mism == 0, f"{mism} of {len(rays)} hit records differ"
 
@@ -120,6 +137,9 @@ def test_trace_samples_bitwise(which, w, h, request):
     exact = np.all(gpu == cpu, axis=1) | np.all(np.isnan(gpu) == np.isnan(cpu), axis=1) & np.all(
         (gpu == cpu) | np.isnan(cpu), axis=1)
     frac = exact.mean()
+    REPORT[f"trace_samples_{which}"] = {"samples": int(len(exact)), "bit_exact_fraction": float(frac),
+                                        "gpu_closest": int(gstats.closest_hit_rays),
+                                        "cpu_closest": int(cstats.closest_hit_rays)}
     assert frac >= 0.999, f"only {frac:.5f} of samples bit-exact"
     assert gstats.closest_hit_rays == cstats.closest_hit_rays or frac < 1.0
     diff = np.abs(gpu[:, :3] - cpu[:, :3]).sum() / max(np.abs(cpu[:, :3]).sum(), 1e-30)
@@ -131,6 +151,9 @@ def test_frame_rel_l2(which, w, h, request):
     rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
     gpu, gstats = dev.render(cam, st, fc, w, h)
     cpu, cstats = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=8)
+    REPORT[f"frame_vs_mt_oracle_{which}"] = {"rel_l2": rel_l2(gpu, cpu), "gpu_rays": [int(gstats.closest_hit_rays),
+                                             int(gstats.shadow_rays)], "cpu_rays": [int(cstats.closest_hit_rays),
+                                             int(cstats.shadow_rays)]}
     assert rel_l2(gpu, cpu) <= 1e-3
     assert gstats.samples == cstats.samples == w * h * st.samples_per_pixel
     # ray counts: identical unless a tie flipped a branch somewhere
@@ -147,7 +170,8 @@ def test_frame_bitwise_vs_reference_order(which, w, h, request):
     gpu, _ = dev.render(cam, st, fc, w, h)
     cpu, _ = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1)
     same = np.all(gpu == cpu, axis=2).mean()
-    print(f"{which}: {same:.6f} of pixels bit-identical, rel L2 {rel_l2(gpu, cpu):.3e}")
+    REPORT[f"frame_bitwise_{which}"] = {"pixels_bit_identical": float(same), "rel_l2": rel_l2(gpu, cpu),
+                                        "frame_equal": bool(np.array_equal(gpu, cpu))}
     assert same >= 0.999
     assert rel_l2(gpu, cpu) <= 1e-6
 
@@ -174,3 +198,20 @@ def test_box_filter_and_progressive_frames(c1):
     ob.render(scene.desc(), cam, st, box, 256, 256, rng_mode=0, threads=8, accum=cpu,
               frame_count=st.samples_per_pixel, total_frame_index=1)
     assert rel_l2(acc2, cpu) <= 1e-5
+
+
+def test_golden_frame_hash(rt):
+    """The GPU frame of C1 at 64x64 equals the committed oracle golden frame byte for byte."""
+    import hashlib
+    import json
+    import os
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))["c1_64x64_frame"]
+    scene, cam, st, fc, post = rt.load_preset("c1", 64, 64)
+    dev = rt.DeviceScene(scene, 0)
+    acc, stats = dev.render(cam, st, fc, 64, 64)
+    dev.close()
+    REPORT["golden_c1_64"] = {"sha256_equal": hashlib.sha256(acc.tobytes()).hexdigest() == gold["sha256"],
+                              "rays": [int(stats.closest_hit_rays), int(stats.shadow_rays)],
+                              "golden_rays": [gold["closest"], gold["shadow"]]}
+    assert (stats.closest_hit_rays, stats.shadow_rays) == (gold["closest"], gold["shadow"])
+    assert hashlib.sha256(acc.tobytes()).hexdigest() == gold["sha256"]
