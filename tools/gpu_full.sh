@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU-box sequence for a round checkpoint: parity tests -> full bench (C3) -> rocprofv3 kernel stats.
+# Stops at the first crash/timeout.
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+ROOTDIR=$(pwd)
+TAG=${TAG:-r01}
+mkdir -p gpurun_out
+timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_${TAG}.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu_${TAG}.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 700 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/bench_${TAG}.log 2>&1
+rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_${TAG}.log | cut -c1-1500
+[ $rc -ne 0 ] && exit $rc
+export TMPDIR=/tmp
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOTDIR/gpurun_out/prof_${TAG} -o run -- python3 $ROOTDIR/bench.py ${PROF_ARGS:---steps 1 --warmup 1 --no-cpu-baseline} > gpurun_out/prof_${TAG}.log 2>&1
+rc=$?; echo "rocprof rc=$rc"
+exit $rc
