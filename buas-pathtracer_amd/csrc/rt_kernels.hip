@@ -8,12 +8,14 @@
 //   samplers / RNG         RT/samplers.{h,cpp}        -> rt_dmath.h + sample_1d/2d below
 //   splat_filter           RT/raytracer.cpp:187-259   -> k_splat (float atomics)
 //
-// Wavefront loop: a pool of N in-flight paths lives in
-// HBM as structure-of-arrays.  One iteration = generate -> extend -> shade ->
-// connect -> splat -> bookkeep, every stage a separate kernel over a
-// compacted queue of path slots.  Queue appends are wave-aggregated
-// (__ballot + popcount + one atomic per wavefront).  Paths are regenerated
-// into freed slots every iteration so the pool stays full.
+// Wavefront loop: a pool of N in-flight paths lives in HBM as
+// structure-of-arrays with a state byte per slot.  One iteration = generate ->
+// extend -> shade -> connect -> splat -> bookkeep, each a separate kernel.
+// generate / shade / splat walk the pool in slot order; the two tracers
+// consume compacted queues (extension rays, shadow rays) that those kernels
+// append to with wave-aggregated atomics (__ballot + popcount + one atomic per
+// wavefront).  Paths are regenerated into freed slots every iteration so the
+// pool stays full.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -607,21 +609,23 @@ struct Pool {
     float4* hit;         // t | code | tri | v
     float*  hit_w;
     uint16_t* mstack;    // [64][n]
-    uint32_t* ext_q[2];
-    uint32_t* done_q;
-    uint32_t* free_q;
+    uint8_t*  state;     // S_FREE / S_TRACE / S_DONE per slot
+    uint32_t* ext_q[2];  // extension queues (ping-pong): slots whose ray must be traced
     uint32_t* sh_slot;
     float4*   sh_o;      // o.xyz | w: light id bits
     float4*   sh_d;      // d.xyz | w: max_t
     float4*   sh_c;      // contribution.xyz
 };
 
+// Slot states.  Every per-iteration kernel except the tracers walks the pool in
+// slot order (thread i = slot i): the SoA loads coalesce, and the queues it
+// appends to come out as runs of consecutive slots (one run per wavefront).
+enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2 };
+
 struct Counters {
     uint32_t ext_count[2];
     uint32_t shadow_count;
-    uint32_t done_count;
-    uint32_t free_count;
-    uint32_t freed;
+    uint32_t gen_count;             // free slots that asked for a sample this iteration
     uint32_t cancel;
     uint32_t pad;
     uint32_t fetch[2];              // persistent trace kernels: items handed out (extend, connect)
@@ -671,10 +675,30 @@ RT_D uint32_t wave_append(uint32_t* counter, bool pred) {
     return base + (uint32_t)__popcll(lower);
 }
 
-RT_D uint32_t n_new_paths(const Counters* c) {
-    unsigned long long remaining = c->total_samples - c->next_sample;
-    return (uint32_t)(remaining < (unsigned long long)c->free_count ? remaining : c->free_count);
+// Workgroup-aggregated append: one atomic per workgroup (the guide's single-word
+// rate, ~88 returning atomics/us, made per-wavefront appends of a 2M-slot pool
+// cost ~0.4 ms per launch).  Every thread of the block must call it.  Entries
+// keep slot order within the block.  `scratch` is LDS of >= waves+1 words.
+template <int NT>
+RT_D uint32_t block_append(uint32_t* counter, bool pred, uint32_t* scratch) {
+    constexpr int NW = NT / 64;
+    const uint32_t lane = __lane_id();
+    const uint32_t wave = threadIdx.x / 64;
+    const unsigned long long mask = __ballot(pred);
+    if (lane == 0) scratch[wave] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t total = 0;
+        for (int w = 0; w < NW; ++w) { uint32_t c = scratch[w]; scratch[w] = total; total += c; }
+        scratch[NW] = total ? atomicAdd(counter, total) : 0u;
+    }
+    __syncthreads();
+    const uint32_t pos = scratch[NW] + scratch[wave] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    __syncthreads();     // scratch may be reused by the next append
+    return pos;
 }
+
+RT_D unsigned long long remaining_samples(const Counters* c) { return c->total_samples - c->next_sample; }
 
 // ---- lens (RT/raytracer.cpp:86-123)
 RT_D V2 transform_bokeh_sample(V2 o, float f, float n, float phi_shutter_max) {
@@ -722,20 +746,21 @@ RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return b
 // ======================================================================
 // Kernels
 // ======================================================================
-constexpr int BLOCK = 256;
+constexpr int BLOCK = 512;          // slot-ordered kernels (generate / shade / splat)
 constexpr int EV_SLOTS = 4;     // iterations between host syncs in run_frame
 
 // k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
 __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
                                                     Counters* cnt, int cur) {
-    const uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
-    const uint32_t n_new = n_new_paths(cnt);
-    const bool active = i < n_new;
-    uint32_t slot = 0;
+    __shared__ uint32_t agg[BLOCK / 64 + 1];
+    const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
+    const bool want = slot < pool.n && pool.state[slot] == S_FREE;
+    // free slots claim consecutive sample numbers, one atomic per workgroup
+    const uint32_t claim = block_append<BLOCK>(&cnt->gen_count, want, agg);
+    const bool active = want && (unsigned long long)claim < remaining_samples(cnt);
     bool enqueue = false;
     if (active) {
-        slot = pool.free_q[cnt->free_count - 1u - i];
-        unsigned long long k = cnt->next_sample + i;
+        unsigned long long k = cnt->next_sample + claim;
         uint32_t x, y, s, p = 0;
         if (fp.list_xy) {
             x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
@@ -786,12 +811,11 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         pool.mstack[slot] = (uint16_t)sc.air_id;            // material_stack[0] = &air
         enqueue = st.max_bounce_count > 0;
+        pool.state[slot] = enqueue ? S_TRACE : S_DONE;   // max_bounce_count == 0: nothing to trace
     }
     // new paths go to the current extension queue behind the survivors of the last shade
-    uint32_t pos = wave_append(&cnt->ext_count[cur], active && enqueue);
+    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[cur], active && enqueue, agg);
     if (active && enqueue) pool.ext_q[cur][pos] = slot;
-    uint32_t dpos = wave_append(&cnt->done_count, active && !enqueue);
-    if (active && !enqueue) pool.done_q[dpos] = slot;
 }
 
 // k_trace<false> — intersect_scene for every queued path (RT/intersection.cpp:606-610)
@@ -883,15 +907,14 @@ __global__ void __launch_bounds__(TB) k_trace(DevScene sc, Pool pool, Counters* 
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
 __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur) {
-    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
-    const bool valid = q < cnt->ext_count[cur];
+    __shared__ uint32_t agg[BLOCK / 64 + 1];
+    const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
+    const bool valid = slot < pool.n && pool.state[slot] == S_TRACE;   // traced this iteration
     bool cont = false, done = false, shadow = false;
-    uint32_t slot = 0;
     V3 sh_o = {0, 0, 0}, sh_d = {0, 0, 0}, sh_c = {0, 0, 0};
     float sh_t = 0.0f;
     uint32_t sh_light = 0;
     if (valid) {
-        slot = pool.ext_q[cur][q];
         const float4 o4 = pool.ray_o[slot], d4 = pool.ray_d[slot];
         const float4 t4 = pool.thr[slot], L4 = pool.L[slot], pn4 = pool.prev_n[slot];
         const float4 h4 = pool.hit[slot];
@@ -1053,27 +1076,24 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
     }
     const int nxt = cur ^ 1;
-    uint32_t pos = wave_append(&cnt->ext_count[nxt], cont);
+    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[nxt], cont, agg);
     if (cont) pool.ext_q[nxt][pos] = slot;
-    uint32_t spos = wave_append(&cnt->shadow_count, shadow);
+    uint32_t spos = block_append<BLOCK>(&cnt->shadow_count, shadow, agg);
     if (shadow) {
         pool.sh_slot[spos] = slot;
         pool.sh_o[spos] = make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light));
         pool.sh_d[spos] = make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t);
         pool.sh_c[spos] = make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f);
     }
-    uint32_t dpos = wave_append(&cnt->done_count, done);
-    if (done) pool.done_q[dpos] = slot;
+    if (done) pool.state[slot] = S_DONE;
 }
 
 // k_splat — vignette + splat_filter (RT/raytracer.cpp:469-488, 187-259) with
 // float atomics, then the slot returns to the free list.
 __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Counters* cnt) {
-    const uint32_t q = blockIdx.x*blockDim.x + threadIdx.x;
-    const bool valid = q < cnt->done_count;
-    uint32_t slot = 0;
+    const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
+    const bool valid = slot < pool.n && pool.state[slot] == S_DONE;
     if (valid) {
-        slot = pool.done_q[q];
         const float4 L = pool.L[slot];
         const float vig = pool.thr[slot].w;
         const float2 j = pool.jitter[slot];
@@ -1119,9 +1139,7 @@ __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Coun
             unsafeAtomicAdd(dst + 3, 1.0f);
         }
     }
-    // free the slot: positions after the ones generate consumed this iteration
-    uint32_t pos = wave_append(&cnt->freed, valid);
-    if (valid) pool.free_q[cnt->free_count - n_new_paths(cnt) + pos] = slot;
+    if (valid) pool.state[slot] = S_FREE;
 }
 
 // k_resolve — splat_filter as a gather (RT/raytracer.cpp:187-259, :476-488).
@@ -1188,23 +1206,18 @@ __global__ void __launch_bounds__(RES_TILE*RES_TILE) k_resolve(FrameParams fp) {
 // k_bookkeep — end of iteration: counters roll over (single thread)
 __global__ void k_bookkeep(Counters* cnt, int cur) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint32_t n_new = n_new_paths(cnt);
+    const unsigned long long rem = remaining_samples(cnt);
     cnt->closest_rays += cnt->ext_count[cur];
     cnt->shadow_rays += cnt->shadow_count;
-    cnt->free_count = cnt->free_count - n_new + cnt->freed;
-    cnt->next_sample += n_new;
-    cnt->freed = 0;
+    cnt->next_sample += ((unsigned long long)cnt->gen_count < rem ? (unsigned long long)cnt->gen_count : rem);
+    cnt->gen_count = 0;
     cnt->ext_count[cur] = 0;
     cnt->shadow_count = 0;
-    cnt->done_count = 0;
     cnt->fetch[0] = 0;
     cnt->fetch[1] = 0;
 }
 
-__global__ void k_init_free(uint32_t* free_q, uint32_t n) {
-    uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
-    if (i < n) free_q[i] = n - 1u - i;       // slot 0 handed out first
-}
+
 
 // debug / parity kernel: intersect_scene / intersect_shadow_ray for explicit rays,
 // through the same Traversal step machine as k_trace (one ray per thread).
@@ -1325,8 +1338,7 @@ int ensure_pool(rt_scene* s, uint32_t n) {
     e |= alloc((void**)&p.mstack, 2*64*N);
     e |= alloc((void**)&p.ext_q[0], 4*N);
     e |= alloc((void**)&p.ext_q[1], 4*N);
-    e |= alloc((void**)&p.done_q, 4*N);
-    e |= alloc((void**)&p.free_q, 4*N);
+    e |= alloc((void**)&p.state, N);
     e |= alloc((void**)&p.sh_slot, 4*N);
     e |= alloc((void**)&p.sh_o, 16*N);
     e |= alloc((void**)&p.sh_d, 16*N);
@@ -1357,11 +1369,9 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     Pool pool = s->pool;
     const uint32_t N = pool.n;
     Counters init = {};
-    init.free_count = N;
     init.total_samples = total;
     HIP_OK(hipMemcpyAsync(s->cnt, &init, sizeof(Counters), hipMemcpyHostToDevice, stream));
-    k_init_free<<<(N + BLOCK - 1) / BLOCK, BLOCK, 0, stream>>>(pool.free_q, N);
-    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemsetAsync(pool.state, S_FREE, N, stream));
     const uint32_t grid = (N + BLOCK - 1) / BLOCK;
     double kms[RT_KERNEL_COUNT] = {};
     uint64_t klaunch[RT_KERNEL_COUNT] = {};
