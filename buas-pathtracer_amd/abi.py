@@ -227,9 +227,13 @@ def bind(lib, table):
 _LIB = None
 
 
-def load_library(path=LIB_PATH):
-    """Load librt_mi355x.so.  There is no fallback: a missing library is an error."""
+def load_library(path=None):
+    """Load librt_mi355x.so.  There is no fallback: a missing library is an error.
+
+    RT_MI355X_LIB names another build of the same library (tuning variants)."""
     global _LIB
+    if path is None:
+        path = os.environ.get("RT_MI355X_LIB") or LIB_PATH
     if _LIB is None:
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: run __graft_entry__.build() (make -C buas-pathtracer_amd/csrc)")

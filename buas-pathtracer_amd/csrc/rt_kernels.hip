@@ -60,6 +60,7 @@ struct DevScene {
     uint32_t light_count;
     const rt_bvh_node* bvh;
     const uint32_t* bvh_idx;
+    const float4* leaf_rec;         // [bvh_index_count][LEAF_REC_Q]: everything a top-level leaf step needs
     uint32_t bvh_node_count;
     const DevMesh* meshes;
     const float4* tris;             // 3 float4 per triangle: a, b-a, c-a (BVH order, all meshes)
@@ -200,6 +201,37 @@ RT_D void load_child_boxes(const rt_bvh_node* nodes, uint32_t left, V3& p0, V3& 
     p1 = {c.x, c.y, c.z}; r1 = {c.w, d.x, d.y};
 }
 
+// A stack entry carries the node's own traversal record, so a pop needs no node
+// load (the parent already loaded it to box-test it):
+//   bit 31 = 0: bit 30 = leaf; leaf: bits 25-29 = count (1..31), bits 0-24 = first;
+//               interior: bits 28-29 = split axis, bits 0-27 = left child
+//   bit 31 = 1: bits 0-30 = node index (the record does not fit; the pop loads the node)
+__host__ __device__ inline uint32_t pack_node(uint32_t idx, uint32_t lf, uint32_t cnt, uint32_t axis) {
+    if (cnt) {
+        if (cnt < 32u && lf < (1u << 25)) return (1u << 30) | (cnt << 25) | lf;
+    } else if (axis < 4u && lf < (1u << 28)) {
+        return (axis << 28) | lf;
+    }
+    return 0x80000000u | idx;
+}
+RT_D void unpack_node(const rt_bvh_node* nodes, uint32_t x, uint32_t& lf, uint32_t& cnt, uint32_t& ax) {
+    if (x & 0x80000000u) {
+        V3 p, r;
+        load_node(nodes, x & 0x7FFFFFFFu, p, r, lf, cnt, ax);
+    } else if (x & (1u << 30)) {
+        cnt = (x >> 25) & 31u; lf = x & 0x1FFFFFFu; ax = 0;
+    } else {
+        cnt = 0; ax = (x >> 28) & 3u; lf = x & 0x0FFFFFFFu;
+    }
+}
+
+// Top-level leaf record (one per bvh_indices slot, built at upload): the
+// primitive's inverse transform, type and size, and for a mesh its offsets and
+// root node, so a top-level leaf step is one round of independent loads.
+//   q0-q2: inverse rows | q3: prim id, type, p[0], p[1] | q4: p[2], node_off, tri_off, root record
+//   q5: root bv_p.xyz, bv_r.x | q6: bv_r.y, bv_r.z
+constexpr int LEAF_REC_Q = 8;
+
 // ----------------------------------------------------------------------
 // Scene traversal as a step machine.
 //
@@ -221,7 +253,13 @@ RT_D void load_child_boxes(const rt_bvh_node* nodes, uint32_t left, V3& p0, V3& 
 // the reference's node_stack[64] (:261, :445).
 // ----------------------------------------------------------------------
 constexpr int STACK_DEPTH = 64;
-constexpr int STACK_LDS = 16;
+#ifndef RT_STACK_LDS
+#define RT_STACK_LDS 16
+#endif
+#ifndef RT_TRI_BATCH
+#define RT_TRI_BATCH 2
+#endif
+constexpr int STACK_LDS = RT_STACK_LDS;
 
 struct Hit {
     float t;
@@ -246,50 +284,70 @@ struct Stack {
 
 enum { TM_TOP = 0, TM_LEAF = 1, TM_MESH = 2, TM_DONE = 3 };
 
+// Each step is: pops (LDS only) until the lane holds a node that survives the
+// far-clip test, ONE round of independent global loads for whatever the lane
+// does next (a sibling pair of nodes, up to TRI_FETCH triangles of a leaf, or a
+// top-level leaf record), then the arithmetic.  Lanes doing different kinds of
+// work in the same step therefore share one memory latency.
+constexpr uint32_t TRI_FETCH = RT_TRI_BATCH;
+constexpr int FETCH_Q = (3*TRI_FETCH > 7u ? 3*TRI_FETCH : 7u);   // float4 per lane per step
+
 template <bool OCC>
 struct Traversal {
-    Ray wr;             // world ray
+    V3 wo, wd;          // world ray
     V3 co, cd, cinv;    // current ray (object space while in a mesh)
-    uint32_t cneg, czero;
+    uint32_t cflags;    // current ray: d < 0 per axis (bits 0-2) | d == 0 per axis (bits 3-5, mesh only)
     float t;
     uint32_t code, tri;
     float hv, hw;
     uint32_t ignored;
-    int sp, mode;
-    uint32_t leaf_first, leaf_count, leaf_i;
-    uint32_t inst, node_off, tri_off;
-    int mesh_base;
-    uint32_t mtri;
-    float mv, mw;
-    bool occluded;
+    int sp, mode, mesh_base;
+    uint32_t leaf_cur, leaf_end;        // TM_LEAF: range of bvh_indices slots still to test
+    uint32_t inst, node_off, tri_off;   // TM_MESH: the instance
+    uint32_t cur_lf, cur_cnt, cur_ax;   // node held by the lane (cur_cnt: leaf size, 0 interior)
+    bool has_cur, occluded;
 
-    RT_D void push_children(const Stack& st, const rt_bvh_node* nodes, uint32_t lf, uint32_t ax) {
-        V3 p0, r0, p1, r1;
-        load_child_boxes(nodes, lf, p0, r0, p1, r1);
-        Ray r; r.o = co; r.d = cd; r.inv_d = cinv; r.zero = czero;
+    RT_D Ray cur_ray() const {
+        Ray r; r.o = co; r.d = cd; r.inv_d = cinv; r.neg = cflags & 7u; r.zero = cflags >> 3; r.max_t = 0.0f;
+        return r;
+    }
+    // Pruning stays off for the world ray: the top level holds box primitives, whose own
+    // slab test (ray_intersect_box) inherits the NaN quirk and can report a hit far away.
+    RT_D void set_world() {
+        const Ray w = make_ray(wo, wd, 0.0f);
+        co = wo; cd = wd; cinv = w.inv_d; cflags = w.neg;
+    }
+
+    RT_D void push(const Stack& st, uint32_t rec, float tn) { if (sp < STACK_DEPTH) st.put(sp++, rec, tn); }
+
+    // children of an interior node from the fetched sibling pair F[0..3]
+    RT_D void push_children(const Stack& st, const float4* F) {
+        const V3 p0 = {F[0].x, F[0].y, F[0].z}, r0 = {F[0].w, F[1].x, F[1].y};
+        const V3 p1 = {F[2].x, F[2].y, F[2].z}, r1 = {F[2].w, F[3].x, F[3].y};
+        const uint32_t ca0 = __float_as_uint(F[1].w), ca1 = __float_as_uint(F[3].w);
+        const uint32_t e0 = pack_node(cur_lf, __float_as_uint(F[1].z), ca0 & 0xFFFFu, ca0 >> 16);
+        const uint32_t e1 = pack_node(cur_lf + 1, __float_as_uint(F[3].z), ca1 & 0xFFFFu, ca1 >> 16);
+        const Ray r = cur_ray();
         float tn0, tn1;
         const bool h0 = bv_static(r, p0, r0, tn0);
         const bool h1 = bv_static(r, p1, r1, tn1);
         // the reference pushes (left, left+1) or (left+1, left); the second is popped first
-        if (!((cneg >> ax) & 1u)) {
-            if (h1 && sp < STACK_DEPTH) st.put(sp++, lf + 1, tn1);
-            if (h0 && sp < STACK_DEPTH) st.put(sp++, lf, tn0);
+        if (!(((cflags & 7u) >> cur_ax) & 1u)) {
+            if (h1) push(st, e1, tn1);
+            if (h0) push(st, e0, tn0);
         } else {
-            if (h0 && sp < STACK_DEPTH) st.put(sp++, lf, tn0);
-            if (h1 && sp < STACK_DEPTH) st.put(sp++, lf + 1, tn1);
+            if (h0) push(st, e0, tn0);
+            if (h1) push(st, e1, tn1);
         }
     }
 
-    // Pruning stays off for the world ray: the top level holds box primitives, whose own
-    // slab test (ray_intersect_box) inherits the NaN quirk and can report a hit far away.
-    RT_D void set_world() { co = wr.o; cd = wr.d; cinv = wr.inv_d; cneg = wr.neg; czero = 0u; }
-
     RT_D void init(const DevScene& sc, const Stack& st, V3 o, V3 d, float max_t, uint32_t ign) {
-        wr = make_ray(o, d, max_t);
-        wr.zero = 0u;
+        wo = o; wd = d;
         set_world();
         t = max_t; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
-        ignored = ign; sp = 0; mode = TM_TOP; occluded = false;
+        ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false;
+        Ray wr = make_ray(o, d, max_t);
+        wr.zero = 0u;                                              // no pruning on the world ray
         for (uint32_t i = 0; i < sc.plane_count; ++i) {            // planes, brute force (:424-433)
             const rt_primitive& pl = sc.planes[i];
             if (ray_plane(wr, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], t)) {
@@ -301,80 +359,101 @@ struct Traversal {
             V3 p, r; uint32_t lf, cnt, ax;
             load_node(sc.bvh, 0, p, r, lf, cnt, ax);
             float tn;
-            if (bv_static(wr, p, r, tn)) st.put(sp++, 0u, tn);
+            if (bv_static(wr, p, r, tn)) st.put(sp++, pack_node(0u, lf, cnt, ax), tn);
         }
+    }
+
+    // pop until an entry above `base` survives the far-clip test (the reference's pop-time
+    // ray_intersect_bounding_volume against the current t); false when none is left
+    RT_D bool pop(const Stack& st, const rt_bvh_node* nodes, int base) {
+        while (sp > base) {
+            const uint2 e = st.get(--sp);
+            if (__uint_as_float(e.y) < t) {
+                unpack_node(nodes, e.x, cur_lf, cur_cnt, cur_ax);
+                has_cur = true;
+                return true;
+            }
+        }
+        return false;
     }
 
     // One traversal step; returns false once the query is finished (mode == TM_DONE).
     RT_D bool step(const DevScene& sc, const Stack& st) {
-        if (mode == TM_MESH) {
-            if (sp == mesh_base) {                                 // instance finished
-                if (mtri != 0xFFFFFFFFu) { code = inst; tri = mtri; hv = mv; hw = mw; }
-                mode = TM_LEAF;
-                set_world();
-                return true;
-            }
-            const uint2 e = st.get(--sp);
-            if (!(__uint_as_float(e.y) < t)) return true;
-            const rt_bvh_node* mn_ = sc.mnodes + node_off;
-            V3 np, nr; uint32_t lf, cnt, ax;
-            load_node(mn_, e.x, np, nr, lf, cnt, ax);
-            if (cnt) {
-                Ray r; r.o = co; r.d = cd;
-                const uint32_t g0 = tri_off + lf;
-                for (uint32_t k = 0; k < cnt; ++k) {
-                    const float4* tp = sc.tris + 3*(size_t)(g0 + k);
-                    const float4 ta = tp[0], tb = tp[1], tc = tp[2];
-                    float v, w;
-                    if (ray_triangle(r, ld3(ta), ld3(tb), ld3(tc), t, v, w)) {
-                        if (OCC) { occluded = true; mode = TM_DONE; return false; }
-                        mtri = g0 + k; mv = v; mw = w;
-                    }
-                }
-            } else {
-                push_children(st, mn_, lf, ax);
-            }
-            return true;
+        // 1. state changes that need no global memory
+        if (mode == TM_MESH && !has_cur && !pop(st, sc.mnodes + node_off, mesh_base)) {
+            mode = TM_LEAF;                                        // instance finished
+            set_world();
         }
+        if (mode == TM_LEAF && leaf_cur == leaf_end) mode = TM_TOP;
+        if (mode == TM_TOP) {
+            if (!has_cur && !pop(st, sc.bvh, 0)) { mode = TM_DONE; return false; }
+            if (cur_cnt) {                                         // top-level leaf: its primitives in order
+                leaf_cur = cur_lf; leaf_end = cur_lf + cur_cnt; has_cur = false;
+                mode = TM_LEAF;
+            }
+        }
+        // 2. one round of loads
+        const float4* src;
+        uint32_t nq;
         if (mode == TM_LEAF) {
-            if (leaf_i == leaf_count) { mode = TM_TOP; return true; }
-            const uint32_t pi = sc.bvh_idx[leaf_first + leaf_i++];
+            src = sc.leaf_rec + (size_t)leaf_cur*LEAF_REC_Q; nq = 7;
+        } else if (cur_cnt) {                                      // mesh leaf
+            src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
+        } else {                                                   // interior: the sibling pair
+            src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4;
+        }
+        float4 F[FETCH_Q];
+#pragma unroll
+        for (int j = 0; j < FETCH_Q; ++j) if ((uint32_t)j < nq) F[j] = src[j];
+        // 3. arithmetic
+        if (mode == TM_LEAF) {
+            const uint32_t pi = __float_as_uint(F[3].x);
+            ++leaf_cur;
             if (pi == ignored) return true;
-            const rt_primitive prim = sc.prims[pi];
-            const M34 inv = load_m34(&sc.inv[prim.transform_index]);
-            Ray ir = make_ray(xform(inv, wr.o, 1.0f), xform(inv, wr.d, 0.0f), wr.max_t);   // transform_ray :403-409
-            if (prim.type == RT_PRIMITIVE_MESH) {                 // intersect_mesh :243-401
-                const DevMesh mesh = sc.meshes[prim.mesh_index];
-                co = ir.o; cd = ir.d; cinv = ir.inv_d; cneg = ir.neg; czero = ir.zero;
-                inst = pi; node_off = mesh.node_offset; tri_off = mesh.tri_offset;
-                mesh_base = sp; mtri = 0xFFFFFFFFu;
-                V3 rp, rr; uint32_t rlf, rcnt, rax;
-                load_node(sc.mnodes + node_off, 0, rp, rr, rlf, rcnt, rax);
+            const uint32_t type = __float_as_uint(F[3].y);
+            M34 inv;
+            inv.e[0][0] = F[0].x; inv.e[0][1] = F[0].y; inv.e[0][2] = F[0].z; inv.e[0][3] = F[0].w;
+            inv.e[1][0] = F[1].x; inv.e[1][1] = F[1].y; inv.e[1][2] = F[1].z; inv.e[1][3] = F[1].w;
+            inv.e[2][0] = F[2].x; inv.e[2][1] = F[2].y; inv.e[2][2] = F[2].z; inv.e[2][3] = F[2].w;
+            const Ray ir = make_ray(xform(inv, wo, 1.0f), xform(inv, wd, 0.0f), 0.0f);   // transform_ray :403-409
+            if (type == RT_PRIMITIVE_MESH) {                      // intersect_mesh :243-401
+                co = ir.o; cd = ir.d; cinv = ir.inv_d; cflags = ir.neg | (ir.zero << 3);
+                inst = pi; node_off = __float_as_uint(F[4].y); tri_off = __float_as_uint(F[4].z);
+                mesh_base = sp;
+                const V3 rp = {F[5].x, F[5].y, F[5].z}, rr = {F[5].w, F[6].x, F[6].y};
                 float tn;
-                if (sp < STACK_DEPTH && bv_static(ir, rp, rr, tn)) st.put(sp++, 0u, tn);
+                if (bv_static(ir, rp, rr, tn)) push(st, __float_as_uint(F[4].w), tn);
                 mode = TM_MESH;
                 return true;
             }
             bool hit = false;
-            if (prim.type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, prim.p[0], t);
-            else if (prim.type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {prim.p[0], prim.p[1], prim.p[2]}, t);
+            if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, F[3].z, t);
+            else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {F[3].z, F[3].w, F[4].x}, t);
             if (hit) {
                 if (OCC) { occluded = true; mode = TM_DONE; return false; }
                 code = pi;
             }
             return true;
         }
-        if (mode == TM_TOP) {
-            if (sp == 0) { mode = TM_DONE; return false; }
-            const uint2 e = st.get(--sp);
-            if (!(__uint_as_float(e.y) < t)) return true;
-            V3 p, r; uint32_t lf, cnt, ax;
-            load_node(sc.bvh, e.x, p, r, lf, cnt, ax);
-            if (cnt) { leaf_first = lf; leaf_count = cnt; leaf_i = 0; mode = TM_LEAF; }
-            else push_children(st, sc.bvh, lf, ax);
+        if (cur_cnt) {                                             // mesh leaf: triangles in order
+            Ray r; r.o = co; r.d = cd;
+            const uint32_t g0 = tri_off + cur_lf;
+#pragma unroll
+            for (uint32_t j = 0; j < TRI_FETCH; ++j)
+                if (j < cur_cnt) {
+                    float v, w;
+                    if (ray_triangle(r, ld3(F[3*j]), ld3(F[3*j + 1]), ld3(F[3*j + 2]), t, v, w)) {
+                        if (OCC) { occluded = true; mode = TM_DONE; return false; }
+                        code = inst; tri = g0 + j; hv = v; hw = w;   // t only decreases: closest so far
+                    }
+                }
+            if (cur_cnt > TRI_FETCH) { cur_lf += TRI_FETCH; cur_cnt -= TRI_FETCH; }
+            else has_cur = false;
             return true;
         }
-        return false;
+        push_children(st, F);
+        has_cur = false;
+        return true;
     }
 
     RT_D Hit result() const {
@@ -615,6 +694,9 @@ struct Pool {
     float4*   sh_o;      // o.xyz | w: light id bits
     float4*   sh_d;      // d.xyz | w: max_t
     float4*   sh_c;      // contribution.xyz
+    uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
+    uint32_t* free_n;    // [blocks]: free slots per BLOCK-slot block after k_splat
+    uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
 };
 
 // Slot states.  Every per-iteration kernel except the tracers walks the pool in
@@ -622,13 +704,19 @@ struct Pool {
 // appends to come out as runs of consecutive slots (one run per wavefront).
 enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2 };
 
+// Queues and fetch heads are sharded NSHARD ways (shard = blockIdx % NSHARD, the
+// blocks that share an XCD), each counter on a 128-B line of its own: one word
+// saturates at ~88 returning atomics/us, and a 2M-slot pool has 4096 blocks.
+constexpr int NSHARD = 8;
+constexpr int LINE_WORDS = 32;
 struct Counters {
-    uint32_t ext_count[2];
-    uint32_t shadow_count;
-    uint32_t gen_count;             // free slots that asked for a sample this iteration
+    uint32_t ext_count[2][NSHARD][LINE_WORDS];   // extension queue length per shard (ping-pong)
+    uint32_t shadow_count[NSHARD][LINE_WORDS];   // shadow queue length per shard
+    uint32_t fetch[2][NSHARD][LINE_WORDS];       // persistent trace kernels: items handed out (extend, connect)
+    uint32_t gen_free;              // free slots counted by the last k_bookkeep = claims of the next k_generate
+    uint32_t pending;               // paths queued for the next iteration (host termination test)
     uint32_t cancel;
     uint32_t pad;
-    uint32_t fetch[2];              // persistent trace kernels: items handed out (extend, connect)
     uint32_t max_steps[2];          // diagnostics: longest traversal (steps) per kind
     float    worst_ray[2][8];       // o.xyz, d.xyz, max_t, steps of a ray above the step threshold
     unsigned long long next_sample;
@@ -675,10 +763,33 @@ RT_D uint32_t wave_append(uint32_t* counter, bool pred) {
     return base + (uint32_t)__popcll(lower);
 }
 
-// Workgroup-aggregated append: one atomic per workgroup (the guide's single-word
-// rate, ~88 returning atomics/us, made per-wavefront appends of a 2M-slot pool
-// cost ~0.4 ms per launch).  Every thread of the block must call it.  Entries
-// keep slot order within the block.  `scratch` is LDS of >= waves+1 words.
+// Workgroup-level exclusive rank of `pred` in thread order; *total = the block's
+// count.  Every thread of the block must call it.  `scratch` is LDS of >= waves+1
+// words; it is free again when the call returns.
+template <int NT>
+RT_D uint32_t block_rank(bool pred, uint32_t* scratch, uint32_t* total) {
+    constexpr int NW = NT / 64;
+    const uint32_t lane = __lane_id();
+    const uint32_t wave = threadIdx.x / 64;
+    const unsigned long long mask = __ballot(pred);
+    if (lane == 0) scratch[wave] = (uint32_t)__popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int w = 0; w < NW; ++w) { uint32_t c = scratch[w]; scratch[w] = t; t += c; }
+        scratch[NW] = t;
+    }
+    __syncthreads();
+    const uint32_t r = scratch[wave] + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    *total = scratch[NW];
+    __syncthreads();
+    return r;
+}
+
+// Workgroup-aggregated append: one atomic per workgroup on the block's shard of
+// the counter (the guide's single-word rate, ~88 returning atomics/us, made
+// per-wavefront appends of a 2M-slot pool cost ~0.4 ms per launch).  Every
+// thread of the block must call it.  Entries keep slot order within the block.
 template <int NT>
 RT_D uint32_t block_append(uint32_t* counter, bool pred, uint32_t* scratch) {
     constexpr int NW = NT / 64;
@@ -755,8 +866,10 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
     __shared__ uint32_t agg[BLOCK / 64 + 1];
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const bool want = slot < pool.n && pool.state[slot] == S_FREE;
-    // free slots claim consecutive sample numbers, one atomic per workgroup
-    const uint32_t claim = block_append<BLOCK>(&cnt->gen_count, want, agg);
+    // free slots claim consecutive sample numbers in slot order: the block's first
+    // claim is the scan of the free counts k_bookkeep made (no atomics)
+    uint32_t nfree;
+    const uint32_t claim = pool.claim_base[blockIdx.x] + block_rank<BLOCK>(want, agg, &nfree);
     const bool active = want && (unsigned long long)claim < remaining_samples(cnt);
     bool enqueue = false;
     if (active) {
@@ -814,8 +927,9 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
         pool.state[slot] = enqueue ? S_TRACE : S_DONE;   // max_bounce_count == 0: nothing to trace
     }
     // new paths go to the current extension queue behind the survivors of the last shade
-    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[cur], active && enqueue, agg);
-    if (active && enqueue) pool.ext_q[cur][pos] = slot;
+    const uint32_t shard = blockIdx.x % NSHARD;
+    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[cur][shard][0], active && enqueue, agg);
+    if (active && enqueue) pool.ext_q[cur][shard*pool.shard_cap + pos] = slot;
 }
 
 // k_trace<false> — intersect_scene for every queued path (RT/intersection.cpp:606-610)
@@ -829,14 +943,23 @@ constexpr int TB = 256;
 constexpr uint32_t CHUNK = 256;
 constexpr int STEPS_PER_REFILL = 8;
 
+#ifdef RT_TRACE_WAVES
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
+#else
+#define RT_TRACE_ATTR
+#endif
 template <bool OCC>
-__global__ void __launch_bounds__(TB) k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill) {
+__global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag) {
     __shared__ uint2 lds_stack[STACK_LDS*TB];
     Stack st;
     st.lds = lds_stack; st.spill = spill; st.lane = threadIdx.x; st.block = TB;
     st.gtid = blockIdx.x*TB + threadIdx.x; st.nthreads = gridDim.x*TB;
-    const uint32_t count = OCC ? cnt->shadow_count : cnt->ext_count[cur];
-    uint32_t* fetch = &cnt->fetch[OCC ? 1 : 0];
+    __shared__ uint32_t qlen[NSHARD];
+    if (threadIdx.x < NSHARD) qlen[threadIdx.x] = OCC ? cnt->shadow_count[threadIdx.x][0] : cnt->ext_count[cur][threadIdx.x][0];
+    __syncthreads();
+    // a wave drains its own shard first, then the others (a plain read of a head
+    // skips exhausted shards without an atomic)
+    uint32_t shard = blockIdx.x % NSHARD, tried = 0;
     const uint32_t lane = __lane_id();
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     uint32_t chunk_next = 0, chunk_end = 0;
@@ -845,11 +968,13 @@ __global__ void __launch_bounds__(TB) k_trace(DevScene sc, Pool pool, Counters* 
     uint32_t steps = 0;
     Traversal<OCC> tr;
     auto finish = [&]() {
-        atomicMax(&cnt->max_steps[OCC ? 1 : 0], steps);
-        if (steps > 20000u) {
-            float* w = cnt->worst_ray[OCC ? 1 : 0];
-            w[0] = tr.wr.o.x; w[1] = tr.wr.o.y; w[2] = tr.wr.o.z;
-            w[3] = tr.wr.d.x; w[4] = tr.wr.d.y; w[5] = tr.wr.d.z; w[6] = tr.wr.max_t; w[7] = (float)steps;
+        if (diag) {                                   // RT_DEBUG_TRAVERSAL: longest traversals
+            atomicMax(&cnt->max_steps[OCC ? 1 : 0], steps);
+            if (steps > 20000u) {
+                float* w = cnt->worst_ray[OCC ? 1 : 0];
+                w[0] = tr.wo.x; w[1] = tr.wo.y; w[2] = tr.wo.z;
+                w[3] = tr.wd.x; w[4] = tr.wd.y; w[5] = tr.wd.z; w[6] = 0.0f; w[7] = (float)steps;
+            }
         }
         if (OCC) {
             if (!tr.occluded) {
@@ -870,12 +995,26 @@ __global__ void __launch_bounds__(TB) k_trace(DevScene sc, Pool pool, Counters* 
         unsigned long long idle = __ballot(!active);
         while (idle && !exhausted) {
             if (chunk_next >= chunk_end) {
-                uint32_t base = 0;
-                if (lane == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) base = atomicAdd(fetch, CHUNK);
-                base = __shfl(base, __ffsll((long long)__ballot(true)) - 1);
-                if (base >= count) { exhausted = true; break; }
-                chunk_next = base;
-                chunk_end = min(base + CHUNK, count);
+                const int leader = __ffsll((long long)__ballot(true)) - 1;
+                bool got = false;
+                while (tried < NSHARD) {
+                    uint32_t* head = &cnt->fetch[OCC ? 1 : 0][shard][0];
+                    const uint32_t len = qlen[shard];
+                    uint32_t base = 0xFFFFFFFFu;
+                    if (lane == (uint32_t)leader &&
+                        __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < len)
+                        base = atomicAdd(head, CHUNK);
+                    base = __shfl(base, leader);
+                    if (base < len) {
+                        chunk_next = shard*pool.shard_cap + base;
+                        chunk_end = shard*pool.shard_cap + min(base + CHUNK, len);
+                        got = true;
+                        break;
+                    }
+                    shard = (shard + 1) % NSHARD;
+                    ++tried;
+                }
+                if (!got) { exhausted = true; break; }
             }
             const uint32_t avail = chunk_end - chunk_next;
             const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
@@ -1076,9 +1215,10 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
     }
     const int nxt = cur ^ 1;
-    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[nxt], cont, agg);
-    if (cont) pool.ext_q[nxt][pos] = slot;
-    uint32_t spos = block_append<BLOCK>(&cnt->shadow_count, shadow, agg);
+    const uint32_t shard = blockIdx.x % NSHARD;
+    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[nxt][shard][0], cont, agg);
+    if (cont) pool.ext_q[nxt][shard*pool.shard_cap + pos] = slot;
+    uint32_t spos = shard*pool.shard_cap + block_append<BLOCK>(&cnt->shadow_count[shard][0], shadow, agg);
     if (shadow) {
         pool.sh_slot[spos] = slot;
         pool.sh_o[spos] = make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light));
@@ -1140,6 +1280,11 @@ __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Coun
         }
     }
     if (valid) pool.state[slot] = S_FREE;
+    // free slots of this block for the next k_generate's claims (scanned by k_bookkeep)
+    __shared__ uint32_t agg[BLOCK / 64 + 1];
+    uint32_t nfree;
+    (void)block_rank<BLOCK>(slot < pool.n && (valid || pool.state[slot] == S_FREE), agg, &nfree);
+    if (threadIdx.x == 0) pool.free_n[blockIdx.x] = nfree;
 }
 
 // k_resolve — splat_filter as a gather (RT/raytracer.cpp:187-259, :476-488).
@@ -1203,21 +1348,64 @@ __global__ void __launch_bounds__(RES_TILE*RES_TILE) k_resolve(FrameParams fp) {
     fp.accum[(size_t)Y*W + X] = acc;
 }
 
-// k_bookkeep — end of iteration: counters roll over (single thread)
-__global__ void k_bookkeep(Counters* cnt, int cur) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    const unsigned long long rem = remaining_samples(cnt);
-    cnt->closest_rays += cnt->ext_count[cur];
-    cnt->shadow_rays += cnt->shadow_count;
-    cnt->next_sample += ((unsigned long long)cnt->gen_count < rem ? (unsigned long long)cnt->gen_count : rem);
-    cnt->gen_count = 0;
-    cnt->ext_count[cur] = 0;
-    cnt->shadow_count = 0;
-    cnt->fetch[0] = 0;
-    cnt->fetch[1] = 0;
+// k_bookkeep — end of iteration (one workgroup): ray counts, counter roll-over,
+// and the exclusive scan of the per-block free counts that gives every block of
+// the next k_generate its first sample claim.  `first` = before the first
+// iteration (only the scan).
+constexpr int BK_THREADS = 1024;
+__global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int first) {
+    __shared__ uint32_t sc[BK_THREADS];
+    __shared__ uint32_t carry;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) {
+        if (!first) {
+            const unsigned long long rem = remaining_samples(cnt);
+            cnt->next_sample += ((unsigned long long)cnt->gen_free < rem ? (unsigned long long)cnt->gen_free : rem);
+            uint32_t ext = 0, sh = 0, pend = 0;
+            for (int k = 0; k < NSHARD; ++k) {
+                ext += cnt->ext_count[cur][k][0];
+                sh += cnt->shadow_count[k][0];
+                pend += cnt->ext_count[cur ^ 1][k][0];
+                cnt->ext_count[cur][k][0] = 0;
+                cnt->shadow_count[k][0] = 0;
+                cnt->fetch[0][k][0] = 0;
+                cnt->fetch[1][k][0] = 0;
+            }
+            cnt->closest_rays += ext;
+            cnt->shadow_rays += sh;
+            cnt->pending = pend;
+        }
+        carry = 0;
+    }
+    __syncthreads();
+    // exclusive scan, BK_THREADS*4 blocks per pass
+    for (uint32_t base = 0; base < nblocks; base += BK_THREADS*4) {
+        uint32_t v[4], sum = 0;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = base + t*4 + k;
+            v[k] = i < nblocks ? pool.free_n[i] : 0u;
+            sum += v[k];
+        }
+        sc[t] = sum;
+        __syncthreads();
+        for (uint32_t off = 1; off < BK_THREADS; off <<= 1) {       // inclusive Hillis-Steele
+            const uint32_t add = t >= off ? sc[t - off] : 0u;
+            __syncthreads();
+            sc[t] += add;
+            __syncthreads();
+        }
+        uint32_t run = carry + sc[t] - sum;
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t i = base + t*4 + k;
+            if (i < nblocks) pool.claim_base[i] = run;
+            run += v[k];
+        }
+        __syncthreads();
+        if (t == BK_THREADS - 1) carry += sc[t];
+        __syncthreads();
+    }
+    if (t == 0) cnt->gen_free = carry;
 }
-
-
 
 // debug / parity kernel: intersect_scene / intersect_shadow_ray for explicit rays,
 // through the same Traversal step machine as k_trace (one ray per thread).
@@ -1326,6 +1514,12 @@ int ensure_pool(rt_scene* s, uint32_t n) {
     };
     int e = 0;
     size_t N = n;
+    const size_t nblocks = (N + BLOCK - 1) / BLOCK;
+    const size_t cap = (nblocks + NSHARD - 1) / NSHARD * BLOCK;   // a block appends <= BLOCK entries per queue
+    const size_t Q = cap*NSHARD;
+    p.shard_cap = (uint32_t)cap;
+    e |= alloc((void**)&p.free_n, 4*nblocks);
+    e |= alloc((void**)&p.claim_base, 4*nblocks);
     e |= alloc((void**)&p.ray_o, 16*N);
     e |= alloc((void**)&p.ray_d, 16*N);
     e |= alloc((void**)&p.thr, 16*N);
@@ -1336,13 +1530,13 @@ int ensure_pool(rt_scene* s, uint32_t n) {
     e |= alloc((void**)&p.hit, 16*N);
     e |= alloc((void**)&p.hit_w, 4*N);
     e |= alloc((void**)&p.mstack, 2*64*N);
-    e |= alloc((void**)&p.ext_q[0], 4*N);
-    e |= alloc((void**)&p.ext_q[1], 4*N);
+    e |= alloc((void**)&p.ext_q[0], 4*Q);
+    e |= alloc((void**)&p.ext_q[1], 4*Q);
     e |= alloc((void**)&p.state, N);
-    e |= alloc((void**)&p.sh_slot, 4*N);
-    e |= alloc((void**)&p.sh_o, 16*N);
-    e |= alloc((void**)&p.sh_d, 16*N);
-    e |= alloc((void**)&p.sh_c, 16*N);
+    e |= alloc((void**)&p.sh_slot, 4*Q);
+    e |= alloc((void**)&p.sh_o, 16*Q);
+    e |= alloc((void**)&p.sh_d, 16*Q);
+    e |= alloc((void**)&p.sh_c, 16*Q);
     if (e) { free_pool(s); return RT_ERROR_OUT_OF_MEMORY; }
     p.n = n;
     return RT_OK;
@@ -1373,6 +1567,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     HIP_OK(hipMemcpyAsync(s->cnt, &init, sizeof(Counters), hipMemcpyHostToDevice, stream));
     HIP_OK(hipMemsetAsync(pool.state, S_FREE, N, stream));
     const uint32_t grid = (N + BLOCK - 1) / BLOCK;
+    HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pool.free_n, BLOCK, grid, stream));   // N is a multiple of BLOCK
+    k_bookkeep<<<1, BK_THREADS, 0, stream>>>(s->cnt, pool, grid, 0, 1);
     double kms[RT_KERNEL_COUNT] = {};
     uint64_t klaunch[RT_KERNEL_COUNT] = {};
     const bool prof = g_profiling;
@@ -1399,6 +1595,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         npending = 0;
     };
     s->cancel = 0;
+    const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
     uint64_t iters = 0;
     int cur = 0;
     for (;;) {
@@ -1408,18 +1605,18 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         k_generate<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
         stage_end(slot, RT_KERNEL_GENERATE);
         stage_begin(slot, RT_KERNEL_EXTEND);
-        k_trace<false><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill);
+        k_trace<false><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill, diag);
         stage_end(slot, RT_KERNEL_EXTEND);
         stage_begin(slot, RT_KERNEL_SHADE);
         k_shade<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
         stage_end(slot, RT_KERNEL_SHADE);
         stage_begin(slot, RT_KERNEL_CONNECT);
-        k_trace<true><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill);
+        k_trace<true><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill, diag);
         stage_end(slot, RT_KERNEL_CONNECT);
         stage_begin(slot, RT_KERNEL_SPLAT);
         k_splat<<<grid, BLOCK, 0, stream>>>(fp, pool, s->cnt);
         stage_end(slot, RT_KERNEL_SPLAT);
-        k_bookkeep<<<1, 64, 0, stream>>>(s->cnt, cur);
+        k_bookkeep<<<1, BK_THREADS, 0, stream>>>(s->cnt, pool, grid, cur, 0);
         HIP_OK(hipGetLastError());
         ++iters;
         cur ^= 1;
@@ -1428,7 +1625,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             HIP_OK(hipStreamSynchronize(stream));
             harvest();
             const Counters& c = *s->cnt_host;
-            if (c.next_sample >= c.total_samples && c.ext_count[cur] == 0) break;
+            if (c.next_sample >= c.total_samples && c.pending == 0) break;
             if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
             if (iters > 100000) { set_error("wavefront loop did not converge"); return RT_ERROR_DEVICE; }
         }
@@ -1580,6 +1777,31 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         return fail(RT_ERROR_INVALID);
     }
     s->bvh_depth = top_depth + mesh_depth;
+    {   // top-level leaf records, in bvh_indices order
+        auto u2f = [](uint32_t u) { float f; memcpy(&f, &u, 4); return f; };
+        std::vector<float4> rec((size_t)d->bvh_index_count*LEAF_REC_Q, make_float4(0, 0, 0, 0));
+        for (uint32_t j = 0; j < d->bvh_index_count; ++j) {
+            const uint32_t pi = d->bvh_indices[j];
+            const rt_primitive& p = d->primitives[pi];
+            float4* q = rec.data() + (size_t)j*LEAF_REC_Q;
+            const M34& iv = inv[p.transform_index];
+            for (int r = 0; r < 3; ++r) q[r] = make_float4(iv.e[r][0], iv.e[r][1], iv.e[r][2], iv.e[r][3]);
+            q[3] = make_float4(u2f(pi), u2f(p.type), p.p[0], p.p[1]);
+            uint32_t node_off = 0, tri_off = 0, root = 0;
+            rt_bvh_node rn = {};
+            if (p.type == RT_PRIMITIVE_MESH) {
+                const rt_mesh& M = d->meshes[p.mesh_index];
+                node_off = meshes[p.mesh_index].node_offset;
+                tri_off = meshes[p.mesh_index].tri_offset;
+                if (M.node_count) rn = M.nodes[0];
+                root = pack_node(0u, rn.left_first, rn.count, rn.split_axis);
+            }
+            q[4] = make_float4(p.p[2], u2f(node_off), u2f(tri_off), u2f(root));
+            q[5] = make_float4(rn.bv_p.x, rn.bv_p.y, rn.bv_p.z, rn.bv_r.x);
+            q[6] = make_float4(rn.bv_r.y, rn.bv_r.z, 0.0f, 0.0f);
+        }
+        if ((err = upload(s, rec.data(), rec.size(), &ds.leaf_rec))) return fail(err);
+    }
     if ((err = upload(s, meshes.data(), meshes.size(), &ds.meshes))) return fail(err);
     if ((err = upload(s, tris.data(), tris.size(), &ds.tris))) return fail(err);
     if ((err = upload(s, orig.data(), orig.size(), &ds.tri_orig))) return fail(err);
