@@ -228,9 +228,10 @@ RT_D void unpack_node(const rt_bvh_node* nodes, uint32_t x, uint32_t& lf, uint32
 // Top-level leaf record (one per bvh_indices slot, built at upload): the
 // primitive's inverse transform, type and size, and for a mesh its offsets and
 // root node, so a top-level leaf step is one round of independent loads.
-//   q0-q2: inverse rows | q3: prim id, type, p[0], p[1] | q4: p[2], node_off, tri_off, root record
-//   q5: root bv_p.xyz, bv_r.x | q6: bv_r.y, bv_r.z
-constexpr int LEAF_REC_Q = 8;
+//   q0-q2: inverse rows | q3: prim id, type, then
+//   sphere/box: q3.zw = p[0], p[1]; q4.x = p[2]
+//   mesh:       q3.zw = node_off, tri_off; q4 = root record, root bv_p.xyz; q5 = root bv_r.xyz
+constexpr int LEAF_REC_Q = 6;
 
 // ----------------------------------------------------------------------
 // Scene traversal as a step machine.
@@ -290,7 +291,7 @@ enum { TM_TOP = 0, TM_LEAF = 1, TM_MESH = 2, TM_DONE = 3 };
 // top-level leaf record), then the arithmetic.  Lanes doing different kinds of
 // work in the same step therefore share one memory latency.
 constexpr uint32_t TRI_FETCH = RT_TRI_BATCH;
-constexpr int FETCH_Q = (3*TRI_FETCH > 7u ? 3*TRI_FETCH : 7u);   // float4 per lane per step
+constexpr int FETCH_Q = (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u);   // float4 per lane per step
 
 template <bool OCC>
 struct Traversal {
@@ -396,7 +397,7 @@ struct Traversal {
         const float4* src;
         uint32_t nq;
         if (mode == TM_LEAF) {
-            src = sc.leaf_rec + (size_t)leaf_cur*LEAF_REC_Q; nq = 7;
+            src = sc.leaf_rec + (size_t)leaf_cur*LEAF_REC_Q; nq = LEAF_REC_Q;
         } else if (cur_cnt) {                                      // mesh leaf
             src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
         } else {                                                   // interior: the sibling pair
@@ -418,11 +419,11 @@ struct Traversal {
             const Ray ir = make_ray(xform(inv, wo, 1.0f), xform(inv, wd, 0.0f), 0.0f);   // transform_ray :403-409
             if (type == RT_PRIMITIVE_MESH) {                      // intersect_mesh :243-401
                 co = ir.o; cd = ir.d; cinv = ir.inv_d; cflags = ir.neg | (ir.zero << 3);
-                inst = pi; node_off = __float_as_uint(F[4].y); tri_off = __float_as_uint(F[4].z);
+                inst = pi; node_off = __float_as_uint(F[3].z); tri_off = __float_as_uint(F[3].w);
                 mesh_base = sp;
-                const V3 rp = {F[5].x, F[5].y, F[5].z}, rr = {F[5].w, F[6].x, F[6].y};
+                const V3 rp = {F[4].y, F[4].z, F[4].w}, rr = {F[5].x, F[5].y, F[5].z};
                 float tn;
-                if (bv_static(ir, rp, rr, tn)) push(st, __float_as_uint(F[4].w), tn);
+                if (bv_static(ir, rp, rr, tn)) push(st, __float_as_uint(F[4].x), tn);
                 mode = TM_MESH;
                 return true;
             }
@@ -689,7 +690,7 @@ struct Pool {
     float*  hit_w;
     uint16_t* mstack;    // [64][n]
     uint8_t*  state;     // S_FREE / S_TRACE / S_DONE per slot
-    uint32_t* ext_q[2];  // extension queues (ping-pong): slots whose ray must be traced
+    float4*   ext_rec[2];// extension queues (ping-pong), 2 float4 per ray: {o.xyz, slot bits}, {d.xyz, 0}
     uint32_t* sh_slot;
     float4*   sh_o;      // o.xyz | w: light id bits
     float4*   sh_d;      // d.xyz | w: max_t
@@ -872,6 +873,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
     const uint32_t claim = pool.claim_base[blockIdx.x] + block_rank<BLOCK>(want, agg, &nfree);
     const bool active = want && (unsigned long long)claim < remaining_samples(cnt);
     bool enqueue = false;
+    V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
     if (active) {
         unsigned long long k = cnt->next_sample + claim;
         uint32_t x, y, s, p = 0;
@@ -915,6 +917,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
         float vig = dot(rd, fp.cz);
         vig = vig*vig*vig*vig;
         vig = lerpf_(1.0f, vig, st.vignette_strength);
+        nro = jcp; nrd = rd;
         pool.ray_o[slot] = make_float4(jcp.x, jcp.y, jcp.z, __uint_as_float(y*fp.w + x));
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
         pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
@@ -929,7 +932,11 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
     // new paths go to the current extension queue behind the survivors of the last shade
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t pos = block_append<BLOCK>(&cnt->ext_count[cur][shard][0], active && enqueue, agg);
-    if (active && enqueue) pool.ext_q[cur][shard*pool.shard_cap + pos] = slot;
+    if (active && enqueue) {
+        float4* q = pool.ext_rec[cur] + 2*((size_t)shard*pool.shard_cap + pos);
+        q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
+        q[1] = make_float4(nrd.x, nrd.y, nrd.z, 0.0f);
+    }
 }
 
 // k_trace<false> — intersect_scene for every queued path (RT/intersection.cpp:606-610)
@@ -941,7 +948,10 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
 // for 64-wide waves), so lanes do not idle behind the wave's longest ray.
 constexpr int TB = 256;
 constexpr uint32_t CHUNK = 256;
-constexpr int STEPS_PER_REFILL = 8;
+#ifndef RT_STEPS_PER_REFILL
+#define RT_STEPS_PER_REFILL 8
+#endif
+constexpr int STEPS_PER_REFILL = RT_STEPS_PER_REFILL;
 
 #ifdef RT_TRACE_WAVES
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
@@ -985,7 +995,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                 pool.L[slot] = L;
             }
         } else {
-            const uint32_t slot = pool.ext_q[cur][item];
+            const uint32_t slot = item;                       // the path's slot (from the record)
             const Hit h = tr.result();
             pool.hit[slot] = make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v);
             pool.hit_w[slot] = h.w;
@@ -1024,8 +1034,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                     const float4 o = pool.sh_o[item], d = pool.sh_d[item];
                     tr.init(sc, st, ld3(o), ld3(d), d.w, __float_as_uint(o.w));
                 } else {
-                    const uint32_t slot = pool.ext_q[cur][item];
-                    tr.init(sc, st, ld3(pool.ray_o[slot]), ld3(pool.ray_d[slot]), FLT_MAX_, 0u);
+                    const float4* q = pool.ext_rec[cur] + 2*(size_t)item;
+                    const float4 o = q[0], d = q[1];
+                    item = __float_as_uint(o.w);
+                    tr.init(sc, st, ld3(o), ld3(d), FLT_MAX_, 0u);
                 }
                 steps = 0;
                 if (tr.mode == TM_DONE) finish(); else active = true;
@@ -1050,6 +1062,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const bool valid = slot < pool.n && pool.state[slot] == S_TRACE;   // traced this iteration
     bool cont = false, done = false, shadow = false;
+    V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
     V3 sh_o = {0, 0, 0}, sh_d = {0, 0, 0}, sh_c = {0, 0, 0};
     float sh_t = 0.0f;
     uint32_t sh_light = 0;
@@ -1207,6 +1220,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
             done = true;
         }
         cont = !done;
+        nro = ro; nrd = rd;
         pool.ray_o[slot] = make_float4(ro.x, ro.y, ro.z, o4.w);
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, d4.w);
         pool.thr[slot] = make_float4(thr.x, thr.y, thr.z, t4.w);
@@ -1217,7 +1231,11 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
     const int nxt = cur ^ 1;
     const uint32_t shard = blockIdx.x % NSHARD;
     uint32_t pos = block_append<BLOCK>(&cnt->ext_count[nxt][shard][0], cont, agg);
-    if (cont) pool.ext_q[nxt][shard*pool.shard_cap + pos] = slot;
+    if (cont) {
+        float4* q = pool.ext_rec[nxt] + 2*((size_t)shard*pool.shard_cap + pos);
+        q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
+        q[1] = make_float4(nrd.x, nrd.y, nrd.z, 0.0f);
+    }
     uint32_t spos = shard*pool.shard_cap + block_append<BLOCK>(&cnt->shadow_count[shard][0], shadow, agg);
     if (shadow) {
         pool.sh_slot[spos] = slot;
@@ -1530,8 +1548,8 @@ int ensure_pool(rt_scene* s, uint32_t n) {
     e |= alloc((void**)&p.hit, 16*N);
     e |= alloc((void**)&p.hit_w, 4*N);
     e |= alloc((void**)&p.mstack, 2*64*N);
-    e |= alloc((void**)&p.ext_q[0], 4*Q);
-    e |= alloc((void**)&p.ext_q[1], 4*Q);
+    e |= alloc((void**)&p.ext_rec[0], 32*Q);
+    e |= alloc((void**)&p.ext_rec[1], 32*Q);
     e |= alloc((void**)&p.state, N);
     e |= alloc((void**)&p.sh_slot, 4*Q);
     e |= alloc((void**)&p.sh_o, 16*Q);
@@ -1786,19 +1804,18 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             float4* q = rec.data() + (size_t)j*LEAF_REC_Q;
             const M34& iv = inv[p.transform_index];
             for (int r = 0; r < 3; ++r) q[r] = make_float4(iv.e[r][0], iv.e[r][1], iv.e[r][2], iv.e[r][3]);
-            q[3] = make_float4(u2f(pi), u2f(p.type), p.p[0], p.p[1]);
-            uint32_t node_off = 0, tri_off = 0, root = 0;
-            rt_bvh_node rn = {};
             if (p.type == RT_PRIMITIVE_MESH) {
                 const rt_mesh& M = d->meshes[p.mesh_index];
-                node_off = meshes[p.mesh_index].node_offset;
-                tri_off = meshes[p.mesh_index].tri_offset;
+                rt_bvh_node rn = {};
                 if (M.node_count) rn = M.nodes[0];
-                root = pack_node(0u, rn.left_first, rn.count, rn.split_axis);
+                const uint32_t root = pack_node(0u, rn.left_first, rn.count, rn.split_axis);
+                q[3] = make_float4(u2f(pi), u2f(p.type), u2f(meshes[p.mesh_index].node_offset), u2f(meshes[p.mesh_index].tri_offset));
+                q[4] = make_float4(u2f(root), rn.bv_p.x, rn.bv_p.y, rn.bv_p.z);
+                q[5] = make_float4(rn.bv_r.x, rn.bv_r.y, rn.bv_r.z, 0.0f);
+            } else {
+                q[3] = make_float4(u2f(pi), u2f(p.type), p.p[0], p.p[1]);
+                q[4] = make_float4(p.p[2], 0.0f, 0.0f, 0.0f);
             }
-            q[4] = make_float4(p.p[2], u2f(node_off), u2f(tri_off), u2f(root));
-            q[5] = make_float4(rn.bv_p.x, rn.bv_p.y, rn.bv_p.z, rn.bv_r.x);
-            q[6] = make_float4(rn.bv_r.y, rn.bv_r.z, 0.0f, 0.0f);
         }
         if ((err = upload(s, rec.data(), rec.size(), &ds.leaf_rec))) return fail(err);
     }
