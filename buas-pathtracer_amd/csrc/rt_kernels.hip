@@ -333,13 +333,12 @@ struct Traversal {
         const bool h0 = bv_static(r, p0, r0, tn0);
         const bool h1 = bv_static(r, p1, r1, tn1);
         // the reference pushes (left, left+1) or (left+1, left); the second is popped first
-        if (!(((cflags & 7u) >> cur_ax) & 1u)) {
-            if (h1) push(st, e1, tn1);
-            if (h0) push(st, e0, tn0);
-        } else {
-            if (h0) push(st, e0, tn0);
-            if (h1) push(st, e1, tn1);
-        }
+        const bool neg = ((cflags & 7u) >> cur_ax) & 1u;
+        const uint32_t ea = neg ? e0 : e1, eb = neg ? e1 : e0;
+        const float ta = neg ? tn0 : tn1, tb = neg ? tn1 : tn0;
+        const bool ha = neg ? h0 : h1, hb = neg ? h1 : h0;
+        if (ha) push(st, ea, ta);
+        if (hb) push(st, eb, tb);
     }
 
     RT_D void init(const DevScene& sc, const Stack& st, V3 o, V3 d, float max_t, uint32_t ign) {
@@ -403,9 +402,11 @@ struct Traversal {
         } else {                                                   // interior: the sibling pair
             src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4;
         }
+        // unconditional: every array the step reads is padded by FETCH_Q float4 at upload
+        (void)nq;
         float4 F[FETCH_Q];
 #pragma unroll
-        for (int j = 0; j < FETCH_Q; ++j) if ((uint32_t)j < nq) F[j] = src[j];
+        for (int j = 0; j < FETCH_Q; ++j) F[j] = src[j];
         // 3. arithmetic
         if (mode == TM_LEAF) {
             const uint32_t pi = __float_as_uint(F[3].x);
@@ -1753,7 +1754,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     uint32_t top_depth = tree_depth(d->bvh_nodes, d->bvh_node_count);
     for (uint32_t i = 0; i < d->bvh_index_count; ++i)
         if (d->bvh_indices[i] >= d->primitive_count) { set_error("bvh index out of range"); return fail(RT_ERROR_INVALID); }
-    if ((err = upload(s, d->bvh_nodes, d->bvh_node_count, &ds.bvh))) return fail(err);
+    // node, triangle and leaf-record arrays get FETCH_Q float4 of padding: a traversal
+    // step loads FETCH_Q float4 unconditionally
+    std::vector<rt_bvh_node> top_nodes(d->bvh_nodes, d->bvh_nodes + d->bvh_node_count);
+    top_nodes.resize(top_nodes.size() + (FETCH_Q*16 + 31)/32, rt_bvh_node{});
+    if ((err = upload(s, top_nodes.data(), top_nodes.size(), &ds.bvh))) return fail(err);
     if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
     ds.bvh_node_count = d->bvh_node_count;
     // meshes: concatenate, triangles as (a, b-a, c-a) float4 triples
@@ -1817,12 +1822,15 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 q[4] = make_float4(p.p[2], 0.0f, 0.0f, 0.0f);
             }
         }
+        rec.resize(rec.size() + FETCH_Q, make_float4(0, 0, 0, 0));
         if ((err = upload(s, rec.data(), rec.size(), &ds.leaf_rec))) return fail(err);
     }
     if ((err = upload(s, meshes.data(), meshes.size(), &ds.meshes))) return fail(err);
+    tris.resize(tris.size() + FETCH_Q, make_float4(0, 0, 0, 0));
     if ((err = upload(s, tris.data(), tris.size(), &ds.tris))) return fail(err);
     if ((err = upload(s, orig.data(), orig.size(), &ds.tri_orig))) return fail(err);
     if ((err = upload(s, normals.data(), normals.size(), &ds.normals))) return fail(err);
+    mnodes.resize(mnodes.size() + (FETCH_Q*16 + 31)/32, rt_bvh_node{});
     if ((err = upload(s, mnodes.data(), mnodes.size(), &ds.mnodes))) return fail(err);
     if (d->skydome && d->skydome_w && d->skydome_h) {
         if ((err = upload(s, reinterpret_cast<const float*>(d->skydome), 3*(size_t)d->skydome_w*d->skydome_h, &ds.sky))) return fail(err);
