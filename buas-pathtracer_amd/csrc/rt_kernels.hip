@@ -273,13 +273,16 @@ struct Stack {
     uint2* lds;         // [STACK_LDS][block] for this block
     uint2* spill;       // [STACK_DEPTH - STACK_LDS][nthreads] global
     uint32_t lane, block, gtid, nthreads;
+    // LDS_ONLY: the caller knows every level it touches is below STACK_LDS
+    template <bool LDS_ONLY = false>
     RT_D void put(int level, uint32_t node, float tn) const {
         uint2 e = make_uint2(node, __float_as_uint(tn));
-        if (level < STACK_LDS) lds[level*block + lane] = e;
+        if (LDS_ONLY || level < STACK_LDS) lds[level*block + lane] = e;
         else spill[(size_t)(level - STACK_LDS)*nthreads + gtid] = e;
     }
+    template <bool LDS_ONLY = false>
     RT_D uint2 get(int level) const {
-        return level < STACK_LDS ? lds[level*block + lane] : spill[(size_t)(level - STACK_LDS)*nthreads + gtid];
+        return (LDS_ONLY || level < STACK_LDS) ? lds[level*block + lane] : spill[(size_t)(level - STACK_LDS)*nthreads + gtid];
     }
 };
 
@@ -319,9 +322,11 @@ struct Traversal {
         co = wo; cd = wd; cinv = w.inv_d; cflags = w.neg;
     }
 
-    RT_D void push(const Stack& st, uint32_t rec, float tn) { if (sp < STACK_DEPTH) st.put(sp++, rec, tn); }
+    template <bool SH>
+    RT_D void push(const Stack& st, uint32_t rec, float tn) { if (SH || sp < STACK_DEPTH) st.put<SH>(sp++, rec, tn); }
 
     // children of an interior node from the fetched sibling pair F[0..3]
+    template <bool SH>
     RT_D void push_children(const Stack& st, const float4* F) {
         const V3 p0 = {F[0].x, F[0].y, F[0].z}, r0 = {F[0].w, F[1].x, F[1].y};
         const V3 p1 = {F[2].x, F[2].y, F[2].z}, r1 = {F[2].w, F[3].x, F[3].y};
@@ -337,8 +342,8 @@ struct Traversal {
         const uint32_t ea = neg ? e0 : e1, eb = neg ? e1 : e0;
         const float ta = neg ? tn0 : tn1, tb = neg ? tn1 : tn0;
         const bool ha = neg ? h0 : h1, hb = neg ? h1 : h0;
-        if (ha) push(st, ea, ta);
-        if (hb) push(st, eb, tb);
+        if (ha) push<SH>(st, ea, ta);
+        if (hb) push<SH>(st, eb, tb);
     }
 
     RT_D void init(const DevScene& sc, const Stack& st, V3 o, V3 d, float max_t, uint32_t ign) {
@@ -365,9 +370,10 @@ struct Traversal {
 
     // pop until an entry above `base` survives the far-clip test (the reference's pop-time
     // ray_intersect_bounding_volume against the current t); false when none is left
+    template <bool SH>
     RT_D bool pop(const Stack& st, const rt_bvh_node* nodes, int base) {
         while (sp > base) {
-            const uint2 e = st.get(--sp);
+            const uint2 e = st.get<SH>(--sp);
             if (__uint_as_float(e.y) < t) {
                 unpack_node(nodes, e.x, cur_lf, cur_cnt, cur_ax);
                 has_cur = true;
@@ -378,15 +384,22 @@ struct Traversal {
     }
 
     // One traversal step; returns false once the query is finished (mode == TM_DONE).
+    // A step pops before it pushes and pushes at most two entries, so when no lane of
+    // the wave is within two levels of STACK_LDS the whole step stays in LDS.
     RT_D bool step(const DevScene& sc, const Stack& st) {
+        if (__ballot(sp > STACK_LDS - 2) == 0ull) return step_impl<true>(sc, st);
+        return step_impl<false>(sc, st);
+    }
+    template <bool SH>
+    RT_D bool step_impl(const DevScene& sc, const Stack& st) {
         // 1. state changes that need no global memory
-        if (mode == TM_MESH && !has_cur && !pop(st, sc.mnodes + node_off, mesh_base)) {
+        if (mode == TM_MESH && !has_cur && !pop<SH>(st, sc.mnodes + node_off, mesh_base)) {
             mode = TM_LEAF;                                        // instance finished
             set_world();
         }
         if (mode == TM_LEAF && leaf_cur == leaf_end) mode = TM_TOP;
         if (mode == TM_TOP) {
-            if (!has_cur && !pop(st, sc.bvh, 0)) { mode = TM_DONE; return false; }
+            if (!has_cur && !pop<SH>(st, sc.bvh, 0)) { mode = TM_DONE; return false; }
             if (cur_cnt) {                                         // top-level leaf: its primitives in order
                 leaf_cur = cur_lf; leaf_end = cur_lf + cur_cnt; has_cur = false;
                 mode = TM_LEAF;
@@ -424,7 +437,7 @@ struct Traversal {
                 mesh_base = sp;
                 const V3 rp = {F[4].y, F[4].z, F[4].w}, rr = {F[5].x, F[5].y, F[5].z};
                 float tn;
-                if (bv_static(ir, rp, rr, tn)) push(st, __float_as_uint(F[4].x), tn);
+                if (bv_static(ir, rp, rr, tn)) push<SH>(st, __float_as_uint(F[4].x), tn);
                 mode = TM_MESH;
                 return true;
             }
@@ -453,7 +466,7 @@ struct Traversal {
             else has_cur = false;
             return true;
         }
-        push_children(st, F);
+        push_children<SH>(st, F);
         has_cur = false;
         return true;
     }
