@@ -58,7 +58,8 @@ struct DevScene {
     const M34* fwd;                 // per transform: forward (rows 0-2)
     const uint32_t* lights;
     uint32_t light_count;
-    const rt_bvh_node* bvh;
+    const rt_bvh_node* bvh;         // traversal layout: {bv_p, bv_r.x}, {bv_r.yz, packed record, 0} (see pack_node)
+    const rt_bvh_node* bvh_src;     // the caller's layout (records that do not pack)
     const uint32_t* bvh_idx;
     const float4* leaf_rec;         // [bvh_index_count][LEAF_REC_Q]: everything a top-level leaf step needs
     uint32_t bvh_node_count;
@@ -66,7 +67,8 @@ struct DevScene {
     const float4* tris;             // 3 float4 per triangle: a, b-a, c-a (BVH order, all meshes)
     const uint32_t* tri_orig;       // mesh-local original triangle index per BVH slot
     const float* normals;           // 9 floats per triangle, ORIGINAL order (same offsets)
-    const rt_bvh_node* mnodes;      // all mesh BVH nodes (child indices mesh-local)
+    const rt_bvh_node* mnodes;      // all mesh BVH nodes (child indices mesh-local), traversal layout
+    const rt_bvh_node* mnodes_src;  // the same in the caller's layout
     const float* sky;               // 3 floats per pixel
     uint32_t sky_w, sky_h;
     V3 top_sky, bot_sky;
@@ -215,13 +217,13 @@ __host__ __device__ inline uint32_t pack_node(uint32_t idx, uint32_t lf, uint32_
     return 0x80000000u | idx;
 }
 RT_D void unpack_node(const rt_bvh_node* nodes, uint32_t x, uint32_t& lf, uint32_t& cnt, uint32_t& ax) {
-    if (x & 0x80000000u) {
+    const bool leaf = (x >> 30) & 1u;
+    cnt = leaf ? (x >> 25) & 31u : 0u;
+    lf = x & (leaf ? 0x1FFFFFFu : 0x0FFFFFFFu);
+    ax = leaf ? 0u : (x >> 28) & 3u;
+    if (x & 0x80000000u) {                                  // rare: the record did not fit
         V3 p, r;
         load_node(nodes, x & 0x7FFFFFFFu, p, r, lf, cnt, ax);
-    } else if (x & (1u << 30)) {
-        cnt = (x >> 25) & 31u; lf = x & 0x1FFFFFFu; ax = 0;
-    } else {
-        cnt = 0; ax = (x >> 28) & 3u; lf = x & 0x0FFFFFFFu;
     }
 }
 
@@ -310,6 +312,12 @@ struct Traversal {
     uint32_t inst, node_off, tri_off;   // TM_MESH: the instance
     uint32_t cur_lf, cur_cnt, cur_ax;   // node held by the lane (cur_cnt: leaf size, 0 interior)
     bool has_cur, occluded;
+#ifdef RT_STEP_STATS
+    uint32_t stat[8] = {};              // lane steps, wave steps*64, pops, -, interior, leaf, record, rays
+#define RT_STAT(i) (++stat[i])
+#else
+#define RT_STAT(i) ((void)0)
+#endif
 
     RT_D Ray cur_ray() const {
         Ray r; r.o = co; r.d = cd; r.inv_d = cinv; r.neg = cflags & 7u; r.zero = cflags >> 3; r.max_t = 0.0f;
@@ -330,9 +338,7 @@ struct Traversal {
     RT_D void push_children(const Stack& st, const float4* F) {
         const V3 p0 = {F[0].x, F[0].y, F[0].z}, r0 = {F[0].w, F[1].x, F[1].y};
         const V3 p1 = {F[2].x, F[2].y, F[2].z}, r1 = {F[2].w, F[3].x, F[3].y};
-        const uint32_t ca0 = __float_as_uint(F[1].w), ca1 = __float_as_uint(F[3].w);
-        const uint32_t e0 = pack_node(cur_lf, __float_as_uint(F[1].z), ca0 & 0xFFFFu, ca0 >> 16);
-        const uint32_t e1 = pack_node(cur_lf + 1, __float_as_uint(F[3].z), ca1 & 0xFFFFu, ca1 >> 16);
+        const uint32_t e0 = __float_as_uint(F[1].z), e1 = __float_as_uint(F[3].z);   // precomputed records
         const Ray r = cur_ray();
         float tn0, tn1;
         const bool h0 = bv_static(r, p0, r0, tn0);
@@ -361,10 +367,10 @@ struct Traversal {
             }
         }
         if (sc.bvh_node_count) {
-            V3 p, r; uint32_t lf, cnt, ax;
-            load_node(sc.bvh, 0, p, r, lf, cnt, ax);
+            const float4* q = reinterpret_cast<const float4*>(sc.bvh);
+            const float4 a = q[0], b = q[1];
             float tn;
-            if (bv_static(wr, p, r, tn)) st.put(sp++, pack_node(0u, lf, cnt, ax), tn);
+            if (bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn)) st.put(sp++, __float_as_uint(b.z), tn);
         }
     }
 
@@ -374,6 +380,7 @@ struct Traversal {
     RT_D bool pop(const Stack& st, const rt_bvh_node* nodes, int base) {
         while (sp > base) {
             const uint2 e = st.get<SH>(--sp);
+            RT_STAT(2);
             if (__uint_as_float(e.y) < t) {
                 unpack_node(nodes, e.x, cur_lf, cur_cnt, cur_ax);
                 has_cur = true;
@@ -392,14 +399,15 @@ struct Traversal {
     }
     template <bool SH>
     RT_D bool step_impl(const DevScene& sc, const Stack& st) {
+        RT_STAT(0);
         // 1. state changes that need no global memory
-        if (mode == TM_MESH && !has_cur && !pop<SH>(st, sc.mnodes + node_off, mesh_base)) {
+        if (mode == TM_MESH && !has_cur && !pop<SH>(st, sc.mnodes_src + node_off, mesh_base)) {
             mode = TM_LEAF;                                        // instance finished
             set_world();
         }
         if (mode == TM_LEAF && leaf_cur == leaf_end) mode = TM_TOP;
         if (mode == TM_TOP) {
-            if (!has_cur && !pop<SH>(st, sc.bvh, 0)) { mode = TM_DONE; return false; }
+            if (!has_cur && !pop<SH>(st, sc.bvh_src, 0)) { mode = TM_DONE; return false; }
             if (cur_cnt) {                                         // top-level leaf: its primitives in order
                 leaf_cur = cur_lf; leaf_end = cur_lf + cur_cnt; has_cur = false;
                 mode = TM_LEAF;
@@ -409,10 +417,13 @@ struct Traversal {
         const float4* src;
         uint32_t nq;
         if (mode == TM_LEAF) {
+            RT_STAT(6);
             src = sc.leaf_rec + (size_t)leaf_cur*LEAF_REC_Q; nq = LEAF_REC_Q;
         } else if (cur_cnt) {                                      // mesh leaf
+            RT_STAT(5);
             src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
         } else {                                                   // interior: the sibling pair
+            RT_STAT(4);
             src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4;
         }
         // unconditional: every array the step reads is padded by FETCH_Q float4 at upload
@@ -732,6 +743,7 @@ struct Counters {
     uint32_t pending;               // paths queued for the next iteration (host termination test)
     uint32_t cancel;
     uint32_t pad;
+    unsigned long long step_stats[2][8];   // RT_STEP_STATS builds: see k_trace
     uint32_t max_steps[2];          // diagnostics: longest traversal (steps) per kind
     float    worst_ray[2][8];       // o.xyz, d.xyz, max_t, steps of a ray above the step threshold
     unsigned long long next_sample;
@@ -1000,6 +1012,9 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                 w[3] = tr.wd.x; w[4] = tr.wd.y; w[5] = tr.wd.z; w[6] = 0.0f; w[7] = (float)steps;
             }
         }
+#ifdef RT_STEP_STATS
+        ++tr.stat[7];
+#endif
         if (OCC) {
             if (!tr.occluded) {
                 const uint32_t slot = pool.sh_slot[item];
@@ -1060,6 +1075,9 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             idle = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;
+#ifdef RT_STEP_STATS
+        if (lane == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) tr.stat[1] += 64*STEPS_PER_REFILL;
+#endif
         if (active) {
             for (int k = 0; k < STEPS_PER_REFILL; ++k) {
                 ++steps;
@@ -1067,6 +1085,9 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             }
         }
     }
+#ifdef RT_STEP_STATS
+    for (int i = 0; i < 8; ++i) atomicAdd(&cnt->step_stats[OCC ? 1 : 0][i], (unsigned long long)tr.stat[i]);
+#endif
 }
 
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
@@ -1511,6 +1532,19 @@ int upload(rt_scene* s, const T* host, size_t count, const T** out) {
     return RT_OK;
 }
 
+// Device traversal layout of a node array: box unchanged, and in place of
+// left_first / count / split_axis the node's packed stack record.
+std::vector<rt_bvh_node> traversal_layout(const rt_bvh_node* nodes, uint32_t count) {
+    std::vector<rt_bvh_node> out(nodes, nodes + count);
+    for (uint32_t i = 0; i < count; ++i) {
+        const uint32_t rec = pack_node(i, nodes[i].left_first, nodes[i].count, nodes[i].split_axis);
+        memcpy(&out[i].left_first, &rec, 4);
+        out[i].count = 0;
+        out[i].split_axis = 0;
+    }
+    return out;
+}
+
 uint32_t tree_depth(const rt_bvh_node* nodes, uint32_t count) {
     if (!count) return 0;
     uint32_t maxd = 0;
@@ -1667,6 +1701,14 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     harvest();
     if (getenv("RT_DEBUG_TRAVERSAL")) {
         const Counters& c = *s->cnt_host;
+        for (int k = 0; k < 2; ++k) {
+            const unsigned long long* v = c.step_stats[k];
+            if (!v[1]) continue;
+            fprintf(stderr, "[rt] %s step stats: rays %llu lane-steps %llu wave-steps*64 %llu (SIMD eff %.3f) steps/ray %.2f "
+                    "pops/ray %.2f interior/ray %.2f leaf/ray %.2f records/ray %.2f\n",
+                    k ? "shadow" : "closest", v[7], v[0], v[1], (double)v[0]/v[1], (double)v[0]/v[7],
+                    (double)v[2]/v[7], (double)v[4]/v[7], (double)v[5]/v[7], (double)v[6]/v[7]);
+        }
         for (int k = 0; k < 2; ++k)
             fprintf(stderr, "[rt] %s: max steps %u; worst ray o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) max_t=%.9g steps=%.0f\n",
                     k ? "shadow" : "closest", c.max_steps[k], c.worst_ray[k][0], c.worst_ray[k][1], c.worst_ray[k][2],
@@ -1771,7 +1813,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     // step loads FETCH_Q float4 unconditionally
     std::vector<rt_bvh_node> top_nodes(d->bvh_nodes, d->bvh_nodes + d->bvh_node_count);
     top_nodes.resize(top_nodes.size() + (FETCH_Q*16 + 31)/32, rt_bvh_node{});
-    if ((err = upload(s, top_nodes.data(), top_nodes.size(), &ds.bvh))) return fail(err);
+    if ((err = upload(s, top_nodes.data(), top_nodes.size(), &ds.bvh_src))) return fail(err);
+    {
+        std::vector<rt_bvh_node> tl = traversal_layout(top_nodes.data(), (uint32_t)top_nodes.size());
+        if ((err = upload(s, tl.data(), tl.size(), &ds.bvh))) return fail(err);
+    }
     if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
     ds.bvh_node_count = d->bvh_node_count;
     // meshes: concatenate, triangles as (a, b-a, c-a) float4 triples
@@ -1844,7 +1890,17 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     if ((err = upload(s, orig.data(), orig.size(), &ds.tri_orig))) return fail(err);
     if ((err = upload(s, normals.data(), normals.size(), &ds.normals))) return fail(err);
     mnodes.resize(mnodes.size() + (FETCH_Q*16 + 31)/32, rt_bvh_node{});
-    if ((err = upload(s, mnodes.data(), mnodes.size(), &ds.mnodes))) return fail(err);
+    if ((err = upload(s, mnodes.data(), mnodes.size(), &ds.mnodes_src))) return fail(err);
+    {
+        // records are mesh-local: the index form carries the node's index within its mesh
+        std::vector<rt_bvh_node> tl(mnodes.size());
+        for (uint32_t m = 0; m < d->mesh_count; ++m) {
+            const uint32_t off = meshes[m].node_offset, n = d->meshes[m].node_count;
+            std::vector<rt_bvh_node> one = traversal_layout(mnodes.data() + off, n);
+            std::copy(one.begin(), one.end(), tl.begin() + off);
+        }
+        if ((err = upload(s, tl.data(), tl.size(), &ds.mnodes))) return fail(err);
+    }
     if (d->skydome && d->skydome_w && d->skydome_h) {
         if ((err = upload(s, reinterpret_cast<const float*>(d->skydome), 3*(size_t)d->skydome_w*d->skydome_h, &ds.sky))) return fail(err);
         ds.sky_w = d->skydome_w; ds.sky_h = d->skydome_h;
