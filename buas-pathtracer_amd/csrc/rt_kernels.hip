@@ -60,6 +60,7 @@ struct DevScene {
     uint32_t light_count;
     const rt_bvh_node* bvh;         // traversal layout: {bv_p, bv_r.x}, {bv_r.yz, packed record, 0} (see pack_node)
     const rt_bvh_node* bvh_src;     // the caller's layout (records that do not pack)
+    uint32_t bvh_root_rec;          // the top-level root's packed stack record
     const uint32_t* bvh_idx;
     const float4* leaf_rec;         // [bvh_index_count][LEAF_REC_Q]: everything a top-level leaf step needs
     uint32_t bvh_node_count;
@@ -298,6 +299,33 @@ enum { TM_TOP = 0, TM_LEAF = 1, TM_MESH = 2, TM_DONE = 3 };
 constexpr uint32_t TRI_FETCH = RT_TRI_BATCH;
 constexpr int FETCH_Q = (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u);   // float4 per lane per step
 
+// The part of intersect_scene_internal (RT/intersection.cpp:411-598) that needs
+// no BVH: the planes, brute force (:424-433), then the top-level root, which the
+// traversal would pop first (its box test and the far-clip test against t).  It
+// runs where the ray is made (k_generate / k_shade, all lanes busy), so the trace
+// kernels only see rays that enter the BVH, already carrying t and 1/d.
+struct Prologue { float t; uint32_t code; bool occluded, bvh; V3 inv_d; };
+RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ) {
+    Prologue r;
+    Ray wr = make_ray(o, d, max_t);
+    wr.zero = 0u;                                                  // no pruning on the world ray
+    r.t = max_t; r.code = RT_HIT_MISS; r.occluded = false; r.bvh = false; r.inv_d = wr.inv_d;
+    for (uint32_t i = 0; i < sc.plane_count; ++i) {
+        const rt_primitive& pl = sc.planes[i];
+        if (ray_plane(wr, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], r.t)) {
+            r.code = RT_HIT_PLANE_BIT | i;
+            if (occ) { r.occluded = true; return r; }
+        }
+    }
+    if (sc.bvh_node_count) {
+        const float4* q = reinterpret_cast<const float4*>(sc.bvh);
+        const float4 a = q[0], b = q[1];
+        float tn;
+        r.bvh = bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn) && tn < r.t;
+    }
+    return r;
+}
+
 template <bool OCC>
 struct Traversal {
     V3 wo, wd;          // world ray
@@ -372,6 +400,16 @@ struct Traversal {
             float tn;
             if (bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn)) st.put(sp++, __float_as_uint(b.z), tn);
         }
+    }
+
+    // a queued ray: ray_prologue ran where it was made; it enters the BVH at the root
+    // (whose pop-time test is known to pass: -inf < t)
+    RT_D void init_rec(const DevScene& sc, const Stack& st, V3 o, V3 d, V3 inv_d, float t0, uint32_t ign) {
+        wo = o; wd = d; co = o; cd = d; cinv = inv_d;
+        cflags = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+        t = t0; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
+        ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false;
+        st.put(sp++, sc.bvh_root_rec, __uint_as_float(0xFF800000u));
     }
 
     // pop until an entry above `base` survives the far-clip test (the reference's pop-time
@@ -715,10 +753,9 @@ struct Pool {
     float*  hit_w;
     uint16_t* mstack;    // [64][n]
     uint8_t*  state;     // S_FREE / S_TRACE / S_DONE per slot
-    float4*   ext_rec[2];// extension queues (ping-pong), 2 float4 per ray: {o.xyz, slot bits}, {d.xyz, 0}
+    float4*   ext_rec[2];// extension queues (ping-pong), REC_Q float4 per ray: {o, slot}, {d, t after planes}, {1/d, -}
     uint32_t* sh_slot;
-    float4*   sh_o;      // o.xyz | w: light id bits
-    float4*   sh_d;      // d.xyz | w: max_t
+    float4*   sh_rec;    // shadow queue, REC_Q float4 per ray: {o, light id}, {d, max_t}, {1/d, -}
     float4*   sh_c;      // contribution.xyz
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
     uint32_t* free_n;    // [blocks]: free slots per BLOCK-slot block after k_splat
@@ -729,6 +766,7 @@ struct Pool {
 // slot order (thread i = slot i): the SoA loads coalesce, and the queues it
 // appends to come out as runs of consecutive slots (one run per wavefront).
 enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2 };
+constexpr int REC_Q = 3;     // float4 per queued ray record
 
 // Queues and fetch heads are sharded NSHARD ways (shard = blockIdx % NSHARD, the
 // blocks that share an XCD), each counter on a 128-B line of its own: one word
@@ -739,6 +777,8 @@ struct Counters {
     uint32_t ext_count[2][NSHARD][LINE_WORDS];   // extension queue length per shard (ping-pong)
     uint32_t shadow_count[NSHARD][LINE_WORDS];   // shadow queue length per shard
     uint32_t fetch[2][NSHARD][LINE_WORDS];       // persistent trace kernels: items handed out (extend, connect)
+    uint32_t cast[2][NSHARD][LINE_WORDS];        // rays cast this iteration: [0] new paths (k_generate), [1] shadow
+    uint32_t alive[NSHARD][LINE_WORDS];          // paths k_shade continued (each casts a closest ray next iteration)
     uint32_t gen_free;              // free slots counted by the last k_bookkeep = claims of the next k_generate
     uint32_t pending;               // paths queued for the next iteration (host termination test)
     uint32_t cancel;
@@ -836,6 +876,14 @@ RT_D uint32_t block_append(uint32_t* counter, bool pred, uint32_t* scratch) {
     return pos;
 }
 
+// Adds the block's count of `pred` to a counter (one no-return atomic per block).
+template <int NT>
+RT_D void block_count(uint32_t* counter, bool pred, uint32_t* scratch) {
+    uint32_t total;
+    (void)block_rank<NT>(pred, scratch, &total);
+    if (threadIdx.x == 0 && total) atomicAdd(counter, total);
+}
+
 RT_D unsigned long long remaining_samples(const Counters* c) { return c->total_samples - c->next_sample; }
 
 // ---- lens (RT/raytracer.cpp:86-123)
@@ -898,8 +946,9 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
     uint32_t nfree;
     const uint32_t claim = pool.claim_base[blockIdx.x] + block_rank<BLOCK>(want, agg, &nfree);
     const bool active = want && (unsigned long long)claim < remaining_samples(cnt);
-    bool enqueue = false;
+    bool enqueue = false, cast = false;
     V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
+    Prologue pro = {};
     if (active) {
         unsigned long long k = cnt->next_sample + claim;
         uint32_t x, y, s, p = 0;
@@ -952,16 +1001,24 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
         pool.jitter[slot] = make_float2(jx, jy);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         pool.mstack[slot] = (uint16_t)sc.air_id;            // material_stack[0] = &air
-        enqueue = st.max_bounce_count > 0;
-        pool.state[slot] = enqueue ? S_TRACE : S_DONE;   // max_bounce_count == 0: nothing to trace
+        cast = st.max_bounce_count > 0;
+        pool.state[slot] = cast ? S_TRACE : S_DONE;      // max_bounce_count == 0: nothing to trace
+        if (cast) {
+            pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false);
+            pool.hit[slot] = make_float4(pro.t, __uint_as_float(pro.code), 0.0f, 0.0f);
+            pool.hit_w[slot] = 0.0f;
+            enqueue = pro.bvh;
+        }
     }
-    // new paths go to the current extension queue behind the survivors of the last shade
+    // new paths that enter the BVH go to the current extension queue behind the survivors
     const uint32_t shard = blockIdx.x % NSHARD;
-    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[cur][shard][0], active && enqueue, agg);
-    if (active && enqueue) {
-        float4* q = pool.ext_rec[cur] + 2*((size_t)shard*pool.shard_cap + pos);
+    block_count<BLOCK>(&cnt->cast[0][shard][0], cast, agg);
+    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[cur][shard][0], enqueue, agg);
+    if (enqueue) {
+        float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + pos);
         q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
-        q[1] = make_float4(nrd.x, nrd.y, nrd.z, 0.0f);
+        q[1] = make_float4(nrd.x, nrd.y, nrd.z, pro.t);
+        q[2] = make_float4(pro.inv_d.x, pro.inv_d.y, pro.inv_d.z, 0.0f);
     }
 }
 
@@ -1023,7 +1080,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                 L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;   // total_color += ... (:768)
                 pool.L[slot] = L;
             }
-        } else {
+        } else if (tr.code != RT_HIT_MISS) {                  // a BVH hit; else k_shade's plane result stands
             const uint32_t slot = item;                       // the path's slot (from the record)
             const Hit h = tr.result();
             pool.hit[slot] = make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v);
@@ -1059,15 +1116,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
             if (!active && rank < avail) {
                 item = chunk_next + rank;
-                if (OCC) {
-                    const float4 o = pool.sh_o[item], d = pool.sh_d[item];
-                    tr.init(sc, st, ld3(o), ld3(d), d.w, __float_as_uint(o.w));
-                } else {
-                    const float4* q = pool.ext_rec[cur] + 2*(size_t)item;
-                    const float4 o = q[0], d = q[1];
-                    item = __float_as_uint(o.w);
-                    tr.init(sc, st, ld3(o), ld3(d), FLT_MAX_, 0u);
-                }
+                const float4* q = (OCC ? pool.sh_rec : pool.ext_rec[cur]) + REC_Q*(size_t)item;
+                const float4 o = q[0], d = q[1], iv = q[2];
+                if (!OCC) item = __float_as_uint(o.w);            // the path's slot
+                tr.init_rec(sc, st, ld3(o), ld3(d), ld3(iv), d.w, OCC ? __float_as_uint(o.w) : 0u);
                 steps = 0;
                 if (tr.mode == TM_DONE) finish(); else active = true;
             }
@@ -1096,7 +1148,8 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
     __shared__ uint32_t agg[BLOCK / 64 + 1];
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const bool valid = slot < pool.n && pool.state[slot] == S_TRACE;   // traced this iteration
-    bool cont = false, done = false, shadow = false;
+    bool cont = false, done = false, shadow = false, cast_shadow = false, enq = false;
+    Prologue spro = {}, cpro = {};
     V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
     V3 sh_o = {0, 0, 0}, sh_d = {0, 0, 0}, sh_c = {0, 0, 0};
     float sh_t = 0.0f;
@@ -1222,7 +1275,12 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
                                 sh_d = Lv;
                                 sh_t = dist - 2*EPSILON;
                                 sh_light = lid;
-                                shadow = true;
+                                cast_shadow = true;
+                                // intersect_shadow_ray (:756): planes and the root here; only rays
+                                // that enter the BVH are queued for k_trace<true>
+                                spro = ray_prologue(sc, sh_o, sh_d, sh_t, true);
+                                shadow = !spro.occluded && spro.bvh;
+                                if (!spro.occluded && !spro.bvh) total = add(total, sh_c);   // :768
                             }
                         }
                     }
@@ -1256,6 +1314,12 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
         }
         cont = !done;
         nro = ro; nrd = rd;
+        if (cont) {                                        // next bounce's intersect_scene: planes + root here
+            cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false);
+            pool.hit[slot] = make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f);
+            pool.hit_w[slot] = 0.0f;
+            enq = cpro.bvh;
+        }
         pool.ray_o[slot] = make_float4(ro.x, ro.y, ro.z, o4.w);
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, d4.w);
         pool.thr[slot] = make_float4(thr.x, thr.y, thr.z, t4.w);
@@ -1265,17 +1329,22 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
     }
     const int nxt = cur ^ 1;
     const uint32_t shard = blockIdx.x % NSHARD;
-    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[nxt][shard][0], cont, agg);
-    if (cont) {
-        float4* q = pool.ext_rec[nxt] + 2*((size_t)shard*pool.shard_cap + pos);
+    block_count<BLOCK>(&cnt->alive[shard][0], cont, agg);
+    block_count<BLOCK>(&cnt->cast[1][shard][0], cast_shadow, agg);
+    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[nxt][shard][0], enq, agg);
+    if (enq) {
+        float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + pos);
         q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
-        q[1] = make_float4(nrd.x, nrd.y, nrd.z, 0.0f);
+        q[1] = make_float4(nrd.x, nrd.y, nrd.z, cpro.t);
+        q[2] = make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, 0.0f);
     }
     uint32_t spos = shard*pool.shard_cap + block_append<BLOCK>(&cnt->shadow_count[shard][0], shadow, agg);
     if (shadow) {
         pool.sh_slot[spos] = slot;
-        pool.sh_o[spos] = make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light));
-        pool.sh_d[spos] = make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t);
+        float4* q = pool.sh_rec + REC_Q*(size_t)spos;
+        q[0] = make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light));
+        q[1] = make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t);
+        q[2] = make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, 0.0f);
         pool.sh_c[spos] = make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f);
     }
     if (done) pool.state[slot] = S_DONE;
@@ -1416,9 +1485,12 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             cnt->next_sample += ((unsigned long long)cnt->gen_free < rem ? (unsigned long long)cnt->gen_free : rem);
             uint32_t ext = 0, sh = 0, pend = 0;
             for (int k = 0; k < NSHARD; ++k) {
-                ext += cnt->ext_count[cur][k][0];
-                sh += cnt->shadow_count[k][0];
-                pend += cnt->ext_count[cur ^ 1][k][0];
+                ext += cnt->cast[0][k][0] + cnt->alive[k][0];
+                sh += cnt->cast[1][k][0];
+                pend += cnt->alive[k][0];
+                cnt->cast[0][k][0] = 0;
+                cnt->cast[1][k][0] = 0;
+                cnt->alive[k][0] = 0;
                 cnt->ext_count[cur][k][0] = 0;
                 cnt->shadow_count[k][0] = 0;
                 cnt->fetch[0][k][0] = 0;
@@ -1596,12 +1668,11 @@ int ensure_pool(rt_scene* s, uint32_t n) {
     e |= alloc((void**)&p.hit, 16*N);
     e |= alloc((void**)&p.hit_w, 4*N);
     e |= alloc((void**)&p.mstack, 2*64*N);
-    e |= alloc((void**)&p.ext_rec[0], 32*Q);
-    e |= alloc((void**)&p.ext_rec[1], 32*Q);
+    e |= alloc((void**)&p.ext_rec[0], 16*REC_Q*Q);
+    e |= alloc((void**)&p.ext_rec[1], 16*REC_Q*Q);
     e |= alloc((void**)&p.state, N);
     e |= alloc((void**)&p.sh_slot, 4*Q);
-    e |= alloc((void**)&p.sh_o, 16*Q);
-    e |= alloc((void**)&p.sh_d, 16*Q);
+    e |= alloc((void**)&p.sh_rec, 16*REC_Q*Q);
     e |= alloc((void**)&p.sh_c, 16*Q);
     if (e) { free_pool(s); return RT_ERROR_OUT_OF_MEMORY; }
     p.n = n;
@@ -1816,6 +1887,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     if ((err = upload(s, top_nodes.data(), top_nodes.size(), &ds.bvh_src))) return fail(err);
     {
         std::vector<rt_bvh_node> tl = traversal_layout(top_nodes.data(), (uint32_t)top_nodes.size());
+        ds.bvh_root_rec = tl[0].left_first;
         if ((err = upload(s, tl.data(), tl.size(), &ds.bvh))) return fail(err);
     }
     if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
