@@ -32,7 +32,9 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table
-EXTEND_BYTES_PER_RAY = 48
+# k_extend algorithmic bytes per traced ray: the queued record (o|slot, d|t, 1/d: 48 B) in,
+# the hit record (t, primitive, triangle, v, w: 20 B) out
+EXTEND_BYTES_PER_RAY = 68
 CONFIGS = {
     "c1": dict(preset="c1", w=512, h=512),
     "c2": dict(preset="c2", w=1920, h=1080),
@@ -161,7 +163,7 @@ def main():
     torch.cuda.synchronize(device)
 
     rt.lib().rt_set_profiling(1)
-    closest = shadow = samples = 0
+    closest = shadow = samples = traced = 0
     kms = [0.0] * 6
     kl = [0] * 6
     if distributed:
@@ -173,6 +175,7 @@ def main():
         closest += s.closest_hit_rays
         shadow += s.shadow_rays
         samples += s.samples
+        traced += s.traced_rays[0]
         for k in range(6):
             kms[k] += s.kernel_ms[k]
             kl[k] += s.kernel_launches[k]
@@ -184,7 +187,7 @@ def main():
 
     totals = torch.tensor([closest, shadow, samples], dtype=torch.float64, device=f"cuda:{device}")
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
-    ext = torch.tensor([kms[1], kl[1], closest], dtype=torch.float64, device=f"cuda:{device}")
+    ext = torch.tensor([kms[1], kl[1], traced], dtype=torch.float64, device=f"cuda:{device}")
     if distributed:
         dist.all_reduce(totals, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -236,7 +239,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": "k_extend", "bytes_per_ray": EXTEND_BYTES_PER_RAY,
                          "mean_launch_ms": round(mean_launch_s * 1e3, 4),
-                         "rays_per_launch": round(rays_per_launch, 1)},
+                         "traced_rays_per_launch": round(rays_per_launch, 1)},
             "stage_ms_per_step": {n: round(kms[i] / args.steps, 2) for i, n in
                                   enumerate(["generate", "extend", "shade", "connect", "splat", "resolve"])},
             "cpu_baseline": cpu,

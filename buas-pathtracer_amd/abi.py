@@ -123,13 +123,15 @@ class TileSet(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("closest_hit_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
                 ("iterations", C.c_uint64), ("seconds", C.c_double),
-                ("kernel_ms", C.c_double * RT_KERNEL_COUNT), ("kernel_launches", C.c_uint64 * RT_KERNEL_COUNT)]
+                ("kernel_ms", C.c_double * RT_KERNEL_COUNT), ("kernel_launches", C.c_uint64 * RT_KERNEL_COUNT),
+                ("traced_rays", C.c_uint64 * 2)]
 
     def as_dict(self):
         return {"closest_hit_rays": self.closest_hit_rays, "shadow_rays": self.shadow_rays,
                 "samples": self.samples, "iterations": self.iterations, "seconds": self.seconds,
                 "kernel_ms": {RT_KERNEL_NAMES[i]: self.kernel_ms[i] for i in range(6)},
-                "kernel_launches": {RT_KERNEL_NAMES[i]: self.kernel_launches[i] for i in range(6)}}
+                "kernel_launches": {RT_KERNEL_NAMES[i]: self.kernel_launches[i] for i in range(6)},
+                "traced_rays": [self.traced_rays[0], self.traced_rays[1]]}
 
 
 class RayQuery(C.Structure):

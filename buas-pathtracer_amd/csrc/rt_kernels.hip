@@ -24,6 +24,7 @@
 #include <vector>
 #include <chrono>
 #include <algorithm>
+#include <cmath>
 
 #include "rt_dmath.h"
 
@@ -61,6 +62,7 @@ struct DevScene {
     const rt_bvh_node* bvh;         // traversal layout: {bv_p, bv_r.x}, {bv_r.yz, packed record, 0} (see pack_node)
     const rt_bvh_node* bvh_src;     // the caller's layout (records that do not pack)
     uint32_t bvh_root_rec;          // the top-level root's packed stack record
+    uint32_t finite_boxes;          // every node box within 2^40 of the origin (finite_box_ray)
     const uint32_t* bvh_idx;
     const float4* leaf_rec;         // [bvh_index_count][LEAF_REC_Q]: everything a top-level leaf step needs
     uint32_t bvh_node_count;
@@ -145,6 +147,9 @@ RT_D bool ray_box(const Ray& ray, V3 br, float& t) {               // :76-105
 // top level holds box primitives whose ray_intersect_box (:76-105) has the
 // same NaN quirk and reports hits the reference keeps (tests/test_gpu_parity.py
 // checks axis-parallel rays against the unpruned oracle).
+// FINITE: the caller guarantees no slab value is NaN (finite_box_ray below), so the
+// reference's ternary max/min chains equal v_max3/v_min3 (a +-0 difference compares equal).
+template <bool FINITE = false>
 RT_D bool bv_static(const Ray& ray, V3 p, V3 r, float& tn_out) {
     V3 rel = sub(ray.o, p);
     V3 m = ray.inv_d;
@@ -152,11 +157,17 @@ RT_D bool bv_static(const Ray& ray, V3 p, V3 r, float& tn_out) {
     V3 k = mul(vabs(m), r);
     V3 t1 = sub(neg(n), k);
     V3 t2 = add(neg(n), k);
-    float tn = mx(mx(t1.x, t1.y), t1.z);
-    float tf = mn(mn(t2.x, t2.y), t2.z);
+    float tn, tf;
+    if (FINITE) {
+        tn = fmaxf(fmaxf(t1.x, t1.y), t1.z);
+        tf = fminf(fminf(t2.x, t2.y), t2.z);
+    } else {
+        tn = mx(mx(t1.x, t1.y), t1.z);
+        tf = mn(mn(t2.x, t2.y), t2.z);
+    }
     tn_out = tn;
     bool hit = (tn < tf) && (tf > 0.0f);
-    if (hit && ray.zero) {
+    if (!FINITE && hit && ray.zero) {
         // margin: 1 % of the node's largest half extent (a triangle's barycentric error is
         // relative to its own size, which the box bounds) plus 1e-5 of its position
         const float margin = 0.01f*mx(r.x, mx(r.y, r.z)) + 1e-5f*mx(fabsf(p.x), mx(fabsf(p.y), fabsf(p.z)));
@@ -165,6 +176,13 @@ RT_D bool bv_static(const Ray& ray, V3 p, V3 r, float& tn_out) {
         if ((ray.zero & 4u) && fabsf(rel.z) > r.z + margin) hit = false;
     }
     return hit;
+}
+// Slab values stay finite when |1/d| <= 2^40, |o| <= 2^40 and every box of the scene
+// lies within 2^40 of the origin (DevScene::finite_boxes): |o - p| * |1/d| < 2^81.
+constexpr float FINITE_LIM = 1099511627776.0f;   // 2^40
+RT_D bool finite_box_ray(V3 o, V3 inv_d) {
+    return fabsf(inv_d.x) <= FINITE_LIM && fabsf(inv_d.y) <= FINITE_LIM && fabsf(inv_d.z) <= FINITE_LIM &&
+           fabsf(o.x) <= FINITE_LIM && fabsf(o.y) <= FINITE_LIM && fabsf(o.z) <= FINITE_LIM;
 }
 RT_D bool ray_triangle(const Ray& ray, V3 a, V3 e1, V3 e2, float& t, float& ov, float& ow) {   // :135-182
     const float eps = 0.000000001f;
@@ -331,6 +349,7 @@ struct Traversal {
     V3 wo, wd;          // world ray
     V3 co, cd, cinv;    // current ray (object space while in a mesh)
     uint32_t cflags;    // current ray: d < 0 per axis (bits 0-2) | d == 0 per axis (bits 3-5, mesh only)
+                        // | bit 6: finite slabs (finite_box_ray and DevScene::finite_boxes)
     float t;
     uint32_t code, tri;
     float hv, hw;
@@ -339,7 +358,7 @@ struct Traversal {
     uint32_t leaf_cur, leaf_end;        // TM_LEAF: range of bvh_indices slots still to test
     uint32_t inst, node_off, tri_off;   // TM_MESH: the instance
     uint32_t cur_lf, cur_cnt, cur_ax;   // node held by the lane (cur_cnt: leaf size, 0 interior)
-    bool has_cur, occluded;
+    bool has_cur, occluded, finite_world;
 #ifdef RT_STEP_STATS
     uint32_t stat[8] = {};              // lane steps, wave steps*64, pops, -, interior, leaf, record, rays
 #define RT_STAT(i) (++stat[i])
@@ -355,22 +374,22 @@ struct Traversal {
     // slab test (ray_intersect_box) inherits the NaN quirk and can report a hit far away.
     RT_D void set_world() {
         const Ray w = make_ray(wo, wd, 0.0f);
-        co = wo; cd = wd; cinv = w.inv_d; cflags = w.neg;
+        co = wo; cd = wd; cinv = w.inv_d; cflags = w.neg | (finite_world ? 64u : 0u);
     }
 
     template <bool SH>
     RT_D void push(const Stack& st, uint32_t rec, float tn) { if (SH || sp < STACK_DEPTH) st.put<SH>(sp++, rec, tn); }
 
     // children of an interior node from the fetched sibling pair F[0..3]
-    template <bool SH>
+    template <bool SH, bool FIN>
     RT_D void push_children(const Stack& st, const float4* F) {
         const V3 p0 = {F[0].x, F[0].y, F[0].z}, r0 = {F[0].w, F[1].x, F[1].y};
         const V3 p1 = {F[2].x, F[2].y, F[2].z}, r1 = {F[2].w, F[3].x, F[3].y};
         const uint32_t e0 = __float_as_uint(F[1].z), e1 = __float_as_uint(F[3].z);   // precomputed records
         const Ray r = cur_ray();
         float tn0, tn1;
-        const bool h0 = bv_static(r, p0, r0, tn0);
-        const bool h1 = bv_static(r, p1, r1, tn1);
+        const bool h0 = bv_static<FIN>(r, p0, r0, tn0);
+        const bool h1 = bv_static<FIN>(r, p1, r1, tn1);
         // the reference pushes (left, left+1) or (left+1, left); the second is popped first
         const bool neg = ((cflags & 7u) >> cur_ax) & 1u;
         const uint32_t ea = neg ? e0 : e1, eb = neg ? e1 : e0;
@@ -382,6 +401,7 @@ struct Traversal {
 
     RT_D void init(const DevScene& sc, const Stack& st, V3 o, V3 d, float max_t, uint32_t ign) {
         wo = o; wd = d;
+        finite_world = false;                                      // debug path: reference max/min chains
         set_world();
         t = max_t; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
         ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false;
@@ -406,7 +426,8 @@ struct Traversal {
     // (whose pop-time test is known to pass: -inf < t)
     RT_D void init_rec(const DevScene& sc, const Stack& st, V3 o, V3 d, V3 inv_d, float t0, uint32_t ign) {
         wo = o; wd = d; co = o; cd = d; cinv = inv_d;
-        cflags = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+        finite_world = sc.finite_boxes && finite_box_ray(o, inv_d);
+        cflags = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u) | (finite_world ? 64u : 0u);
         t = t0; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
         ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false;
         st.put(sp++, sc.bvh_root_rec, __uint_as_float(0xFF800000u));
@@ -432,10 +453,10 @@ struct Traversal {
     // A step pops before it pushes and pushes at most two entries, so when no lane of
     // the wave is within two levels of STACK_LDS the whole step stays in LDS.
     RT_D bool step(const DevScene& sc, const Stack& st) {
-        if (__ballot(sp > STACK_LDS - 2) == 0ull) return step_impl<true>(sc, st);
-        return step_impl<false>(sc, st);
+        if (__ballot(sp > STACK_LDS - 2 || !(cflags & 64u)) == 0ull) return step_impl<true, true>(sc, st);
+        return step_impl<false, false>(sc, st);
     }
-    template <bool SH>
+    template <bool SH, bool FIN>
     RT_D bool step_impl(const DevScene& sc, const Stack& st) {
         RT_STAT(0);
         // 1. state changes that need no global memory
@@ -481,7 +502,8 @@ struct Traversal {
             inv.e[2][0] = F[2].x; inv.e[2][1] = F[2].y; inv.e[2][2] = F[2].z; inv.e[2][3] = F[2].w;
             const Ray ir = make_ray(xform(inv, wo, 1.0f), xform(inv, wd, 0.0f), 0.0f);   // transform_ray :403-409
             if (type == RT_PRIMITIVE_MESH) {                      // intersect_mesh :243-401
-                co = ir.o; cd = ir.d; cinv = ir.inv_d; cflags = ir.neg | (ir.zero << 3);
+                co = ir.o; cd = ir.d; cinv = ir.inv_d;
+                cflags = ir.neg | (ir.zero << 3) | ((sc.finite_boxes && finite_box_ray(ir.o, ir.inv_d)) ? 64u : 0u);
                 inst = pi; node_off = __float_as_uint(F[3].z); tri_off = __float_as_uint(F[3].w);
                 mesh_base = sp;
                 const V3 rp = {F[4].y, F[4].z, F[4].w}, rr = {F[5].x, F[5].y, F[5].z};
@@ -515,7 +537,7 @@ struct Traversal {
             else has_cur = false;
             return true;
         }
-        push_children<SH>(st, F);
+        push_children<SH, FIN>(st, F);
         has_cur = false;
         return true;
     }
@@ -790,6 +812,7 @@ struct Counters {
     unsigned long long total_samples;
     unsigned long long closest_rays;
     unsigned long long shadow_rays;
+    unsigned long long traced_rays[2];   // handed to k_trace<false> / k_trace<true>
 };
 
 struct FrameParams {
@@ -1483,11 +1506,13 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         if (!first) {
             const unsigned long long rem = remaining_samples(cnt);
             cnt->next_sample += ((unsigned long long)cnt->gen_free < rem ? (unsigned long long)cnt->gen_free : rem);
-            uint32_t ext = 0, sh = 0, pend = 0;
+            uint32_t ext = 0, sh = 0, pend = 0, tq = 0, ts = 0;
             for (int k = 0; k < NSHARD; ++k) {
                 ext += cnt->cast[0][k][0] + cnt->alive[k][0];
                 sh += cnt->cast[1][k][0];
                 pend += cnt->alive[k][0];
+                tq += cnt->ext_count[cur][k][0];
+                ts += cnt->shadow_count[k][0];
                 cnt->cast[0][k][0] = 0;
                 cnt->cast[1][k][0] = 0;
                 cnt->alive[k][0] = 0;
@@ -1498,6 +1523,8 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             }
             cnt->closest_rays += ext;
             cnt->shadow_rays += sh;
+            cnt->traced_rays[0] += tq;
+            cnt->traced_rays[1] += ts;
             cnt->pending = pend;
         }
         carry = 0;
@@ -1793,6 +1820,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         stats->iterations = iters;
         stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int k = 0; k < RT_KERNEL_COUNT; ++k) { stats->kernel_ms[k] = kms[k]; stats->kernel_launches[k] = klaunch[k]; }
+        stats->traced_rays[0] = s->cnt_host->traced_rays[0];
+        stats->traced_rays[1] = s->cnt_host->traced_rays[1];
     }
     return RT_OK;
 }
@@ -1925,6 +1954,17 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 normals.push_back(nn.x); normals.push_back(nn.y); normals.push_back(nn.z);
             }
         mnodes.insert(mnodes.end(), M.nodes, M.nodes + M.node_count);
+    }
+    {   // finite_box_ray's scene condition: every box within 2^40 of the origin
+        auto within = [](const rt_bvh_node* n, size_t count) {
+            for (size_t i = 0; i < count; ++i) {
+                const float c[3] = {n[i].bv_p.x, n[i].bv_p.y, n[i].bv_p.z}, r[3] = {n[i].bv_r.x, n[i].bv_r.y, n[i].bv_r.z};
+                for (int k = 0; k < 3; ++k)
+                    if (!(std::fabs(c[k]) + std::fabs(r[k]) <= 1099511627776.0f)) return false;   // NaN fails too
+            }
+            return true;
+        };
+        ds.finite_boxes = (within(d->bvh_nodes, d->bvh_node_count) && within(mnodes.data(), mnodes.size())) ? 1u : 0u;
     }
     if (top_depth + mesh_depth + 2 > STACK_DEPTH) {
         set_error("BVH too deep for the 64-entry traversal stack (RT/intersection.cpp:445)");

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- status */
 enum rt_status {
@@ -207,6 +207,9 @@ typedef struct rt_stats {
        launches, measured on the stream the stage kernels run on */
     double   kernel_ms[RT_KERNEL_COUNT];
     uint64_t kernel_launches[RT_KERNEL_COUNT];
+    /* rays handed to the trace kernels (closest, shadow): the rest were settled by
+       the planes / top-level root test where they were made (GPU only) */
+    uint64_t traced_rays[2];
 } rt_stats;
 
 typedef struct rt_ray_query {       /* debug/parity entry: one ray for rt_debug_intersect */

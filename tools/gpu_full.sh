@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU-box sequence for a round checkpoint: parity tests -> full bench (C3) -> rocprofv3 kernel stats.
+# GPU-box sequence for a round checkpoint: parity tests -> full bench (C3) -> rocprofv3 kernel stats
+# of the same workload -> PMC passes (FETCH_SIZE, WRITE_SIZE) for the HBM traffic of k_extend.
 # Stops at the first crash/timeout.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 ROOTDIR=$(pwd)
@@ -12,6 +13,16 @@ timeout -k 10 700 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > gpurun_o
 rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench_${TAG}.log | cut -c1-1500
 [ $rc -ne 0 ] && exit $rc
 export TMPDIR=/tmp
-timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOTDIR/gpurun_out/prof_${TAG} -o run -- python3 $ROOTDIR/bench.py ${PROF_ARGS:---steps 1 --warmup 1 --no-cpu-baseline} > gpurun_out/prof_${TAG}.log 2>&1
+PA=${PROF_ARGS:---steps 1 --warmup 1 --no-cpu-baseline}
+timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOTDIR/gpurun_out/prof_${TAG} -o run -- python3 $ROOTDIR/bench.py $PA > gpurun_out/prof_${TAG}.log 2>&1
 rc=$?; echo "rocprof rc=$rc"
-exit $rc
+[ $rc -ne 0 ] && exit $rc
+[ -n "$NO_PMC" ] && exit 0
+mkdir -p gpurun_out/pmc_${TAG}
+i=0
+for grp in FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -k 10 500 rocprofv3 --pmc $grp --output-format csv -d $ROOTDIR/gpurun_out/pmc_${TAG}/pass$i -o run -- python3 $ROOTDIR/bench.py $PA > gpurun_out/pmc_${TAG}/pass$i.log 2>&1 || { rc=$?; echo "pmc $grp rc=$rc"; exit $rc; }
+  echo "pmc $grp ok"
+done
+exit 0

@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh output) per kernel.
+
+usage: tools/pmc_summary.py gpurun_out/<TAG> [--out profiles/<name>.md] [--traffic profiles/traffic.json
+                            --bench-log gpurun_out/<TAG>/pass1.log]
+
+Counter values are summed over every dispatch of a kernel; SQ counters on gfx950 are
+summed over the shader engines.  FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM
+section: gfx950 reports half the bytes of a wide coalesced read); both sizes are in KiB.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+
+KERNELS = ["k_generate", "k_trace<false>", "k_shade", "k_trace<true>", "k_splat", "k_resolve", "k_bookkeep"]
+LABEL = {"k_trace<false>": "k_extend (k_trace<false>)", "k_trace<true>": "k_connect (k_trace<true>)"}
+
+
+def short(name):
+    for k in KERNELS:
+        if k in name:
+            return k
+    return None
+
+
+def load(tag_dir):
+    val = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    dur = collections.defaultdict(dict)
+    for f in sorted(glob.glob(os.path.join(tag_dir, "pass*", "**", "*counter_collection.csv"), recursive=True)):
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            if not k:
+                continue
+            key = (f, r["Dispatch_Id"])
+            val[k][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[k].add(key)
+            dur[k][key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3
+    return val, disp, dur
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag_dir")
+    ap.add_argument("--out")
+    ap.add_argument("--traffic")
+    ap.add_argument("--bench-log")
+    a = ap.parse_args()
+    val, disp, dur = load(a.tag_dir)
+    lines = [f"# PMC summary: {a.tag_dir}", "",
+             "Per kernel, summed over dispatches (each pass is a separate bench run; dispatch counts per pass are equal).",
+             "", "| kernel | dispatches/pass | mean us | VALU util | wait (s_waitcnt) | issue-stall | VMEM lat (cyc) |"
+             " L2 hit | L1->L2 req/access | HBM rd MB/launch | HBM wr MB/launch |",
+             "|---|---|---|---|---|---|---|---|---|---|---|"]
+    out = {}
+    npass = max(1, len(glob.glob(os.path.join(a.tag_dir, "pass*", ""))))
+    for k in KERNELS:
+        if k not in val:
+            continue
+        v = val[k]
+        n = len(disp[k]) / npass
+        g = lambda c: v.get(c, float("nan"))
+        wc = g("SQ_WAVE_CYCLES")
+        valu = g("SQ_ACTIVE_INST_VALU") / wc if wc else float("nan")
+        wait = g("SQ_WAIT_ANY") / wc if wc else float("nan")
+        stall = g("SQ_WAIT_INST_ANY") / wc if wc else float("nan")
+        lat = g("SQ_ACCUM_PREV_HIRES") / g("SQ_INSTS_VMEM") if g("SQ_INSTS_VMEM") else float("nan")
+        hit = g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")) if g("TCC_HIT_sum") == g("TCC_HIT_sum") else float("nan")
+        l1 = g("TCP_TCC_READ_REQ_sum") / g("TCP_TOTAL_CACHE_ACCESSES_sum") if g("TCP_TOTAL_CACHE_ACCESSES_sum") else float("nan")
+        rd = 2.0 * g("FETCH_SIZE") * 1024 / n / 1e6
+        wr = g("WRITE_SIZE") * 1024 / n / 1e6
+        mean_us = sum(dur[k].values()) / max(1, len(dur[k]))
+        out[k] = {"dispatches": n, "mean_us": mean_us, "valu_util": valu, "wait_frac": wait, "issue_stall_frac": stall,
+                  "vmem_latency_cycles": lat, "l2_hit": hit, "l1_miss_req_per_access": l1,
+                  "hbm_read_mb_per_launch": rd, "hbm_write_mb_per_launch": wr}
+        lines.append(f"| {LABEL.get(k, k)} | {n:.0f} | {mean_us:.1f} | {valu:.3f} | {wait:.3f} | {stall:.3f} | {lat:.0f} | "
+                     f"{hit:.3f} | {l1:.3f} | {rd:.1f} | {wr:.1f} |")
+    lines += ["", "VALU util = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (per wave); wait = SQ_WAIT_ANY / SQ_WAVE_CYCLES;",
+              "issue-stall = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES; VMEM latency = SQ_ACCUM_PREV_HIRES / SQ_INSTS_VMEM;",
+              "HBM rd = 2 x FETCH_SIZE (gfx950 correction), wr = WRITE_SIZE, per launch."]
+    text = "\n".join(lines) + "\n"
+    print(text)
+    if a.out:
+        open(a.out, "w").write(text)
+        json.dump(out, open(os.path.splitext(a.out)[0] + ".json", "w"), indent=1)
+    if a.traffic and "k_trace<false>" in out:
+        e = out["k_trace<false>"]
+        rec = {"config": "c3", "kernel": "k_extend",
+               "hbm_bytes_per_launch": (e["hbm_read_mb_per_launch"] + e["hbm_write_mb_per_launch"]) * 1e6,
+               "source": a.tag_dir, "note": "2 x FETCH_SIZE + WRITE_SIZE per k_trace<false> launch (rocprofv3 --pmc)"}
+        if a.bench_log and os.path.exists(a.bench_log):
+            for line in open(a.bench_log):
+                if line.startswith("{"):
+                    b = json.loads(line)
+                    rec["bench_spp"] = b["config"].get("spp")
+                    rec["traced_rays_per_launch"] = b["roofline"].get("traced_rays_per_launch", b["roofline"].get("rays_per_launch"))
+        json.dump(rec, open(a.traffic, "w"), indent=1)
+        print("wrote", a.traffic, rec)
+
+
+if __name__ == "__main__":
+    main()
