@@ -211,6 +211,26 @@ def main():
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
+        # output pass on the resolved frame: k_post, 16 B read + 4 B written per pixel
+        bgra = torch.empty((h, w), dtype=torch.int32, device=f"cuda:{device}")
+        pcall = lambda: rt.lib().rt_postprocess_device(device, C.c_void_p(accum.data_ptr()), w, h, C.byref(post), 0,
+                                                       C.c_void_p(bgra.data_ptr()), C.c_void_p(stream.cuda_stream))
+        for _ in range(3):
+            assert pcall() == 0, rt.lib().rt_last_error()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        post_ms = []
+        for _ in range(20):
+            ev[0].record(stream)
+            assert pcall() == 0
+            ev[1].record(stream)
+            ev[1].synchronize()
+            post_ms.append(ev[0].elapsed_time(ev[1]))
+        post_ms = sorted(post_ms)[len(post_ms) // 2]
+        post_gbs = 20.0 * w * h / (post_ms * 1e-3) / 1e9
+        postprocess = {"kernel": "k_post", "ms": round(post_ms, 4), "achieved_GBps": round(post_gbs, 1),
+                       "frac_of_hbm_peak": round(post_gbs / HBM_PEAK_GBS, 4), "bytes_per_pixel": 20,
+                       "note": "median of 20 calls, HIP events on the render stream around each call "
+                               "(includes launch latency); rocprof gives the kernel alone"}
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(rt, cfg, args.spp, args.cpu_seconds)
@@ -243,6 +263,7 @@ def main():
             "stage_ms_per_step": {n: round(kms[i] / args.steps, 2) for i, n in
                                   enumerate(["generate", "extend", "shade", "connect", "splat", "resolve"])},
             "cpu_baseline": cpu,
+            "postprocess": postprocess,
         }
         print(json.dumps(out), flush=True)
     dev.close()

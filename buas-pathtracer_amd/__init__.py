@@ -26,7 +26,7 @@ from .abi import (V3, v3, M4x4Inv, Material, Camera, Settings, FilterCache, Post
 
 __all__ = ["Scene", "DeviceScene", "RenderError", "load_preset", "default_settings", "load_reconstruction_kernel",
            "translate", "scale", "rotate_x", "rotate_y", "rotate_z", "identity", "aim_camera", "aim_camera_at",
-           "recompute_camera", "resolve_bgra8", "write_bitmap", "lib", "abi", "v3", "PI_32", "DEG_TO_RAD"]
+           "recompute_camera", "resolve_bgra8", "postprocess", "write_bitmap", "lib", "abi", "v3", "PI_32", "DEG_TO_RAD"]
 
 PI_32 = 3.14159265359
 DEG_TO_RAD = 6.28318530717 / 360.0
@@ -278,6 +278,18 @@ def resolve_bgra8(accum, post):
     out = np.zeros((h, w), np.uint32)
     buf = AccumulationBuffer(w, h, 0, accum.ctypes.data_as(C.POINTER(C.c_float)))
     lib().rth_resolve_bgra8(C.byref(buf), C.byref(post), out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out
+
+
+def postprocess(accum, post, total_frame_index=0, device=0):
+    """The output pass on the GPU (rt_postprocess; RT/raytracer.cpp:2103-2171): host float4 (h, w, 4) in,
+    BGRA8 (h, w) u32 out, with the reference's TPDF blue-noise dither."""
+    accum = np.ascontiguousarray(accum, np.float32)
+    h, w, _ = accum.shape
+    out = np.zeros((h, w), np.uint32)
+    buf = AccumulationBuffer(w, h, 0, accum.ctypes.data_as(C.POINTER(C.c_float)))
+    _check(lib().rt_postprocess(device, C.byref(buf), C.byref(post), total_frame_index,
+                                out.ctypes.data_as(C.POINTER(C.c_uint32))))
     return out
 
 

@@ -172,6 +172,9 @@ ABI_FUNCTIONS = {
     "rt_set_profiling": (C.c_int, [C.c_int]),
     "rt_set_path_pool": (C.c_int, [C.c_uint32]),
     "rt_cancel": (C.c_int, [C.c_void_p]),
+    "rt_postprocess_device": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, P(PostSettings), C.c_uint32,
+                                        C.c_void_p, C.c_void_p]),
+    "rt_postprocess": (C.c_int, [C.c_int, P(AccumulationBuffer), P(PostSettings), C.c_uint32, P(C.c_uint32)]),
 }
 
 HOST_FUNCTIONS = {

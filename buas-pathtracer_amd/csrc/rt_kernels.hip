@@ -25,6 +25,7 @@
 #include <chrono>
 #include <algorithm>
 #include <cmath>
+#include <mutex>
 
 #include "rt_dmath.h"
 
@@ -42,6 +43,7 @@ uint32_t g_pool_override = 0;
 // Tables embedded from data/ (extracted from the reference by tools/extract_tables.py).
 extern "C" const unsigned char rt_dev_strata_tab[16384];
 extern "C" const unsigned char rt_dev_bluenoise_tab[327680];
+extern "C" const unsigned char rt_dev_dither_tab[8*256*256*3];
 
 // ======================================================================
 // Device scene
@@ -1589,6 +1591,64 @@ __global__ void __launch_bounds__(128) k_debug_intersect(DevScene sc, const rt_r
     out[i] = r;
 }
 
+// k_post — the output pass (RT/raytracer.cpp:2103-2171): resolve, exposure,
+// tonemap, sRGB, contrast, TPDF dither, BGRA8.  One pixel per thread; 16 B in,
+// 4 B out (HBM-bound).  The dither texture (196 KB) stays in L2.
+RT_D float post_clamp(float n, float a, float b) { return mx(a, mn(b, n)); }     // MathLib clamp
+RT_D float sigmoidal_contrast(float x, float contrast, float midpoint) {        // :69-84
+    float curve;
+    if (x < midpoint) {
+        float scale = (1.0f / midpoint)*x;
+        curve = midpoint*(scale*scale);
+    } else {
+        float y = (1.0f / (1.0f - midpoint));
+        float scale = y - y*x;
+        curve = 1.0f - (1.0f - midpoint)*(scale*scale);
+    }
+    return lerpf_(x, curve, contrast);
+}
+RT_D float remap_tpdf(float x) {                                                // :125-132
+    float orig = 2.0f*x - 1.0f;
+    x = orig*(1.0f / __builtin_sqrtf(fabsf(orig)));   // rsqrtss there; correctly rounded here
+    x = mx(-1.0f, x);
+    x = x - sign_of(x);
+    return x;
+}
+__global__ void __launch_bounds__(256) k_post(const float4* px, uint32_t w, uint32_t h, rt_post_settings post,
+                                              const uint8_t* noise, uint32_t* out) {
+    const uint32_t x = blockIdx.x*64 + (threadIdx.x & 63), y = blockIdx.y*4 + (threadIdx.x >> 6);
+    if (x >= w || y >= h) return;
+    const size_t i = (size_t)y*w + x;
+    const float4 s = px[i];
+    V3 c = {0.0f, 0.0f, 0.0f};
+    if ((s.x != s.x) || (s.y != s.y) || (s.z != s.z) || (s.w != s.w)) {
+        c = {0.0f, 255.0f, 255.0f};
+    } else if (s.w > 0.001f) {
+        c = {s.x / s.w, s.y / s.w, s.z / s.w};
+        c = {mx(c.x, 0.0f), mx(c.y, 0.0f), mx(c.z, 0.0f)};
+        if (post.exposure != 0.0f) c = smul(d_powf(2.0f, post.exposure), c);
+        if (post.tonemapping) c = {1.0f - d_expf(-c.x), 1.0f - d_expf(-c.y), 1.0f - d_expf(-c.z)};
+        if (post.srgb_transform) {
+            const float g = 1.0f / 2.23333f;
+            c = {d_powf(c.x, g), d_powf(c.y, g), d_powf(c.z, g)};
+        }
+        if (post.contrast != 0.0f)
+            c = {sigmoidal_contrast(c.x, post.contrast, post.midpoint), sigmoidal_contrast(c.y, post.contrast, post.midpoint),
+                 sigmoidal_contrast(c.z, post.contrast, post.midpoint)};
+        c = smul(255.0f, c);
+        const uint8_t* d = noise + 3*((size_t)(y & 255u)*256 + (x & 255u));
+        c.x = c.x + (0.5f + remap_tpdf((1.0f / 255.0f)*(float)d[0]));
+        c.y = c.y + (0.5f + remap_tpdf((1.0f / 255.0f)*(float)d[1]));
+        c.z = c.z + (0.5f + remap_tpdf((1.0f / 255.0f)*(float)d[2]));
+    } else if (s.w < -0.01f) {
+        c = {-255.0f*s.w, 0.0f, -255.0f*s.w};
+    }
+    const uint32_t r = (uint8_t)post_clamp(c.x, 0.0f, 255.0f);
+    const uint32_t g = (uint8_t)post_clamp(c.y, 0.0f, 255.0f);
+    const uint32_t b = (uint8_t)post_clamp(c.z, 0.0f, 255.0f);
+    out[i] = (255u << 24) | (r << 16) | (g << 8) | b;
+}
+
 // ======================================================================
 // Host side: rt_scene + C ABI
 // ======================================================================
@@ -2056,6 +2116,51 @@ int rt_scene_free(rt_scene* s) {
 }
 
 int rt_cancel(rt_scene* s) { if (s) s->cancel = 1; return RT_OK; }
+
+int rt_postprocess_device(int device, const float* d_pixels, uint32_t w, uint32_t h, const rt_post_settings* post,
+                          uint32_t total_frame_index, uint32_t* d_bgra, void* hip_stream) {
+    if (!d_pixels || !post || !d_bgra || !w || !h) { set_error("null argument"); return RT_ERROR_INVALID; }
+    int err = bind_device(device);
+    if (err) return err;
+    static std::mutex mu;
+    static std::vector<uint8_t*> tabs;                 // per device: the 8 dither textures (1.5 MB)
+    const uint8_t* tab = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if ((int)tabs.size() <= device) tabs.resize(device + 1, nullptr);
+        if (!tabs[device]) {
+            HIP_OK(hipMalloc(&tabs[device], sizeof(rt_dev_dither_tab)));
+            HIP_OK(hipMemcpy(tabs[device], rt_dev_dither_tab, sizeof(rt_dev_dither_tab), hipMemcpyHostToDevice));
+        }
+        tab = tabs[device];
+    }
+    hipStream_t stream = static_cast<hipStream_t>(hip_stream);
+    const dim3 grid((w + 63) / 64, (h + 3) / 4);
+    k_post<<<grid, 256, 0, stream>>>(reinterpret_cast<const float4*>(d_pixels), w, h, *post,
+                                     tab + (size_t)(total_frame_index % 8u)*256*256*3, d_bgra);
+    HIP_OK(hipGetLastError());
+    HIP_OK(hipStreamSynchronize(stream));
+    return RT_OK;
+}
+
+int rt_postprocess(int device, const rt_accumulation_buffer* accum, const rt_post_settings* post,
+                   uint32_t total_frame_index, uint32_t* out_bgra) {
+    if (!accum || !accum->pixels || !post || !out_bgra || !accum->w || !accum->h) { set_error("null argument"); return RT_ERROR_INVALID; }
+    int err = bind_device(device);
+    if (err) return err;
+    const size_t n = (size_t)accum->w*accum->h;
+    float* d_px = nullptr;
+    uint32_t* d_out = nullptr;
+    HIP_OK(hipMalloc(&d_px, 16*n));
+    if (hipMalloc(&d_out, 4*n) != hipSuccess) { (void)hipFree(d_px); set_error("hipMalloc"); return RT_ERROR_OUT_OF_MEMORY; }
+    err = RT_OK;
+    if (hipMemcpy(d_px, accum->pixels, 16*n, hipMemcpyHostToDevice) != hipSuccess) { set_error("hipMemcpy"); err = RT_ERROR_DEVICE; }
+    if (!err) err = rt_postprocess_device(device, d_px, accum->w, accum->h, post, total_frame_index, d_out, nullptr);
+    if (!err && hipMemcpy(out_bgra, d_out, 4*n, hipMemcpyDeviceToHost) != hipSuccess) { set_error("hipMemcpy"); err = RT_ERROR_DEVICE; }
+    (void)hipFree(d_px);
+    (void)hipFree(d_out);
+    return err;
+}
 
 int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st,
                      const rt_filter_cache* filter, const rt_tile_set* tiles,

@@ -171,6 +171,14 @@ typedef struct rt_accumulation_buffer {                        /* RT/Raytracer.h
     float*   pixels;                /* w*h float4 (xyz = weighted radiance, w = weight) */
 } rt_accumulation_buffer;
 
+typedef struct rt_post_settings {   /* PostProcessSettings RT/scene.h:84-90 */
+    float   exposure;               /* stops: colour *= 2^exposure when != 0 */
+    int32_t tonemapping;            /* 1 - exp(-x) */
+    int32_t srgb_transform;         /* x^(1/2.23333) */
+    float   midpoint;               /* sigmoidal_contrast (RT/raytracer.cpp:69-84) */
+    float   contrast;
+} rt_post_settings;
+
 typedef struct rt_tile_set {        /* WorkQueue tiling RT/Raytracer.h:70-91 + sharding */
     uint32_t tile_w, tile_h;        /* 64x64 in the reference (RT/raytracer.cpp:1657) */
     uint32_t shard_index;           /* this GPU renders tiles t with t % shard_count == shard_index */
@@ -271,6 +279,22 @@ int rt_trace_samples(rt_scene* scene, const rt_camera* camera, const rt_settings
  * intersect_shadow_ray (occlusion = 1) for `count` rays (RT/intersection.cpp:600-610). */
 int rt_debug_intersect(rt_scene* scene, uint32_t count, const rt_ray_query* rays,
                        int occlusion, rt_hit_record* out);
+
+/* The output pass of RT/raytracer.cpp:2103-2171 on the device: per pixel resolve
+ * (xyz / w), exposure, 1-exp(-x) tonemap, sRGB power, sigmoidal contrast, x255,
+ * TPDF dither from the reference's LDR_RGB1 blue-noise texture number
+ * total_frame_index % 8 (RT/assets.cpp:63-113), clamp, BGRA8 pack; NaN pixels
+ * become (0,255,255), negative weights magenta.  d_pixels (w*h float4) and d_bgra
+ * (w*h u32) are DEVICE pointers on `device`; `hip_stream` may be NULL.
+ * remap_tpdf's rsqrtss (an approximation whose bits differ between CPU models)
+ * is computed as 1/sqrt, correctly rounded. */
+int rt_postprocess_device(int device, const float* d_pixels, uint32_t w, uint32_t h,
+                          const rt_post_settings* post, uint32_t total_frame_index,
+                          uint32_t* d_bgra, void* hip_stream);
+
+/* Same, from and to host memory (accum->pixels in, out_bgra w*h u32 out). */
+int rt_postprocess(int device, const rt_accumulation_buffer* accum, const rt_post_settings* post,
+                   uint32_t total_frame_index, uint32_t* out_bgra);
 
 /* Record per-stage HIP-event timings into rt_stats::kernel_ms (off by default). */
 int rt_set_profiling(int enable);

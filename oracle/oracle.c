@@ -1409,3 +1409,64 @@ int oracle_load_filter(const char* name, rt_filter_cache* out) {             /* 
     }
     return RT_OK;
 }
+
+/* ======================================================================
+ * Output pass (RT/raytracer.cpp:2103-2171)
+ * ==================================================================== */
+extern const unsigned char rt_dither_rgb1_256[8*256*256*3];   /* data/dither_rgb1_256.u8 */
+
+static float post_clamp(float n, float a, float b) { return mx(a, mn(b, n)); }   /* MathLib clamp */
+
+static float sigmoidal_contrast(float x, float contrast, float midpoint) {      /* RT/raytracer.cpp:69-84 */
+    float curve;
+    if (x < midpoint) {
+        float scale = (1.0f / midpoint)*x;
+        curve = midpoint*(scale*scale);
+    } else {
+        float y = (1.0f / (1.0f - midpoint));
+        float scale = y - y*x;
+        curve = 1.0f - (1.0f - midpoint)*(scale*scale);
+    }
+    return x*(1.0f - contrast) + curve*contrast;                                /* lerp(x, curve, contrast) */
+}
+
+static float remap_tpdf(float x) {                                              /* RT/raytracer.cpp:125-132 */
+    float orig = 2.0f*x - 1.0f;
+    x = orig*(1.0f / sqrtf(fabsf(orig)));       /* fast_approx_inverse_square_root = rsqrtss there */
+    x = mx(-1.0f, x);
+    x = x - (x < 0.0f ? -1.0f : 1.0f);          /* sign_of */
+    return x;
+}
+
+void oracle_postprocess(const rt_accumulation_buffer* a, const rt_post_settings* post,
+                        uint32_t total_frame_index, uint32_t* out) {
+    const unsigned char* noise = rt_dither_rgb1_256 + (size_t)(total_frame_index % 8u)*256*256*3;
+    size_t i = 0;
+    for (uint32_t y = 0; y < a->h; ++y)
+        for (uint32_t x = 0; x < a->w; ++x, ++i) {
+            const float* s = a->pixels + 4*i;
+            float c[3] = {0.0f, 0.0f, 0.0f};
+            if ((s[0] != s[0]) || (s[1] != s[1]) || (s[2] != s[2]) || (s[3] != s[3])) {
+                c[0] = 0.0f; c[1] = 255.0f; c[2] = 255.0f;
+            } else if (s[3] > 0.001f) {
+                for (int k = 0; k < 3; ++k) { c[k] = s[k] / s[3]; c[k] = mx(c[k], 0.0f); }
+                if (post->exposure != 0.0f) {
+                    const float e = powf_(2.0f, post->exposure);
+                    for (int k = 0; k < 3; ++k) c[k] = c[k]*e;
+                }
+                if (post->tonemapping) for (int k = 0; k < 3; ++k) c[k] = 1.0f - expf_(-c[k]);
+                if (post->srgb_transform) for (int k = 0; k < 3; ++k) c[k] = powf_(c[k], 1.0f / 2.23333f);
+                if (post->contrast != 0.0f)
+                    for (int k = 0; k < 3; ++k) c[k] = sigmoidal_contrast(c[k], post->contrast, post->midpoint);
+                for (int k = 0; k < 3; ++k) c[k] = c[k]*255.0f;
+                const unsigned char* d = noise + 3*((size_t)(y & 255u)*256 + (x & 255u));
+                for (int k = 0; k < 3; ++k) c[k] = c[k] + (0.5f + remap_tpdf((1.0f / 255.0f)*(float)d[k]));
+            } else if (s[3] < -0.01f) {
+                c[0] = -255.0f*s[3]; c[1] = 0.0f; c[2] = -255.0f*s[3];
+            }
+            uint32_t r = (uint8_t)post_clamp(c[0], 0.0f, 255.0f);
+            uint32_t g = (uint8_t)post_clamp(c[1], 0.0f, 255.0f);
+            uint32_t b = (uint8_t)post_clamp(c[2], 0.0f, 255.0f);
+            out[i] = (255u << 24) | (r << 16) | (g << 8) | b;
+        }
+}

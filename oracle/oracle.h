@@ -57,6 +57,12 @@ int oracle_trace_samples(const rt_scene_desc* scene, const rt_camera* camera, co
 int oracle_debug_intersect(const rt_scene_desc* scene, uint32_t count, const rt_ray_query* rays,
                            int occlusion, rt_hit_record* out);
 
+/* The output pass (RT/raytracer.cpp:2103-2171): resolve, exposure, tonemap, sRGB,
+ * contrast, TPDF dither (LDR_RGB1 texture total_frame_index % 8), BGRA8.  remap_tpdf's
+ * rsqrtss is 1/sqrtf here (and on the GPU); transcendentals follow oracle_set_math_mode. */
+void oracle_postprocess(const rt_accumulation_buffer* accum, const rt_post_settings* post,
+                        uint32_t total_frame_index, uint32_t* out_bgra);
+
 /* ---- known-answer helpers (unit tests / golden vectors) ---------------- */
 uint32_t oracle_wang_hash(uint32_t key);
 uint32_t oracle_sample_seed(uint32_t total_frame_index, uint32_t frame_count, uint32_t tile_index,

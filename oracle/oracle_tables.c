@@ -19,4 +19,10 @@ __asm__(
     "rt_bluenoise_256spp:\n"
     ".incbin \"" RT_STR(RT_DATA_DIR) "/bluenoise_256spp.u8\"\n"
     ".size rt_bluenoise_256spp, 327680\n"
+    ".global rt_dither_rgb1_256\n"
+    ".type rt_dither_rgb1_256, @object\n"
+    ".balign 64\n"
+    "rt_dither_rgb1_256:\n"
+    ".incbin \"" RT_STR(RT_DATA_DIR) "/dither_rgb1_256.u8\"\n"
+    ".size rt_dither_rgb1_256, 1572864\n"
     ".text\n");

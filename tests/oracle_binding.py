@@ -53,6 +53,7 @@ def load():
         "oracle_asinf": (C.c_float, [C.c_float]),
         "oracle_set_math_mode": (None, [C.c_int]),
         "oracle_load_filter": (C.c_int, [C.c_char_p, P(abi.FilterCache)]),
+        "oracle_postprocess": (None, [P(abi.AccumulationBuffer), P(abi.PostSettings), C.c_uint32, P(C.c_uint32)]),
     }
     for name, (res, args) in fns.items():
         f = getattr(lib, name)
@@ -104,3 +105,16 @@ def intersect(desc, rays, occlusion=False):
     out = (abi.HitRecord * n)()
     assert load().oracle_debug_intersect(C.byref(desc), n, q, int(bool(occlusion)), out) == 0
     return list(out)
+
+
+def postprocess(accum, post, total_frame_index=0):
+    """oracle_postprocess: the reference's output pass (RT/raytracer.cpp:2103-2171) -> BGRA8 (h, w) u32."""
+    import numpy as np
+    import sys
+    abi = sys.modules["buas_pathtracer_amd"].abi
+    accum = np.ascontiguousarray(accum, np.float32)
+    h, w, _ = accum.shape
+    out = np.zeros((h, w), np.uint32)
+    buf = abi.AccumulationBuffer(w, h, 0, accum.ctypes.data_as(C.POINTER(C.c_float)))
+    load().oracle_postprocess(C.byref(buf), C.byref(post), total_frame_index, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out

@@ -215,3 +215,26 @@ def test_golden_frame_hash(rt):
                               "golden_rays": [gold["closest"], gold["shadow"]]}
     assert (stats.closest_hit_rays, stats.shadow_rays) == (gold["closest"], gold["shadow"])
     assert hashlib.sha256(acc.tobytes()).hexdigest() == gold["sha256"]
+
+
+@pytest.mark.parametrize("frame", [0, 5])
+def test_postprocess_bit_exact(c1, frame):
+    """The output pass (k_post via rt_postprocess) equals oracle_postprocess byte for byte
+    (spec transcendentals on both sides) on a rendered frame plus special pixels, for
+    several post settings."""
+    rt, scene, cam, st, fc, dev = c1
+    acc, _ = dev.render(cam, st, fc, 256, 256)
+    acc = acc.copy()
+    acc[0, 0] = [np.nan, 1, 1, 1]
+    acc[0, 1] = [1, 1, 1, 0]
+    acc[0, 2] = [0, 0, 0, -0.75]
+    acc[0, 3] = [1e30, 1, 0, 1]
+    settings = [rt.abi.PostSettings(0.0, 1, 1, 0.5, 0.0), rt.abi.PostSettings(0.75, 1, 1, 0.45, 0.35),
+                rt.abi.PostSettings(-1.0, 0, 0, 0.5, 0.0), rt.abi.PostSettings(0.0, 1, 0, 0.6, 1.0)]
+    same = []
+    for post in settings:
+        gpu = rt.postprocess(acc, post, total_frame_index=frame)
+        cpu = ob.postprocess(acc, post, total_frame_index=frame)
+        same.append(float((gpu == cpu).mean()))
+        assert np.array_equal(gpu, cpu), f"{(gpu != cpu).sum()} pixels differ"
+    REPORT[f"postprocess_frame{frame}"] = {"pixels_bit_identical": same}
