@@ -53,6 +53,36 @@ def c3small(rt):
     dev.close()
 
 
+@pytest.fixture(scope="module")
+def c4small(rt):
+    """C4 topology (4 mesh instances, boxes, 3 sphere lights, nested dielectric shell)."""
+    scene, cam, st, fc, post = rt.load_preset("c4", 192, 108)
+    dev = rt.DeviceScene(scene, 0)
+    yield rt, scene, cam, st, fc, dev
+    dev.close()
+
+
+@pytest.fixture(scope="module")
+def c5small(rt):
+    """C5 sampler: OptimizedBlueNoise; 320 spp so indices past 256 take the stratified fallback
+    (RT/samplers.cpp:27-28)."""
+    scene, cam, st, fc, post = rt.load_preset("c5", 96, 54)
+    st.samples_per_pixel = 320
+    dev = rt.DeviceScene(scene, 0)
+    yield rt, scene, cam, st, fc, dev
+    dev.close()
+
+
+@pytest.fixture(scope="module")
+def c1uniform(rt):
+    """C1 with SamplingStrategy_Uniform (the third sampler)."""
+    scene, cam, st, fc, post = rt.load_preset("c1", 128, 128)
+    st.sampling_strategy = rt.abi.RT_SAMPLING_UNIFORM
+    dev = rt.DeviceScene(scene, 0)
+    yield rt, scene, cam, st, fc, dev
+    dev.close()
+
+
 def random_rays(rng, n, center, spread):
     rays = []
     o = center + spread * (rng.random((n, 3)) - 0.5)
@@ -64,7 +94,7 @@ def random_rays(rng, n, center, spread):
     return rays
 
 
-@pytest.mark.parametrize("which", ["c1", "c3small"])
+@pytest.mark.parametrize("which", ["c1", "c3small", "c4small"])
 @pytest.mark.parametrize("occlusion", [False, True])
 def test_intersect_bit_exact(which, occlusion, request):
     rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
@@ -127,7 +157,8 @@ def _sample_list(rng, w, h, n, spp):
     return xy, s
 
 
-@pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108)])
+@pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108), ("c4small", 192, 108),
+                                       ("c5small", 96, 54), ("c1uniform", 128, 128)])
 def test_trace_samples_bitwise(which, w, h, request):
     rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
     rng = np.random.default_rng(11)
@@ -146,7 +177,8 @@ def test_trace_samples_bitwise(which, w, h, request):
     assert diff <= 1e-3
 
 
-@pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108)])
+@pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108), ("c4small", 192, 108),
+                                       ("c5small", 96, 54), ("c1uniform", 128, 128)])
 def test_frame_rel_l2(which, w, h, request):
     rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
     gpu, gstats = dev.render(cam, st, fc, w, h)
@@ -161,7 +193,8 @@ def test_frame_rel_l2(which, w, h, request):
     assert abs(int(gstats.shadow_rays) - int(cstats.shadow_rays)) <= 1e-4 * cstats.shadow_rays
 
 
-@pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108)])
+@pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108), ("c4small", 192, 108),
+                                       ("c5small", 96, 54), ("c1uniform", 128, 128)])
 def test_frame_bitwise_vs_reference_order(which, w, h, request):
     """k_resolve sums each pixel's contributions in the single-threaded reference
     order, so the GPU frame equals the oracle's threads=1 frame bit for bit

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 ROOTDIR=$(pwd)
 TAG=${TAG:-r01}
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/pytest_gpu_${TAG}.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu_${TAG}.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_gpu_${TAG}.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 700 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/bench_${TAG}.log 2>&1
