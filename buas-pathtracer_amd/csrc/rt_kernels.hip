@@ -64,6 +64,9 @@ struct DevScene {
     const rt_bvh_node* bvh;         // traversal layout: {bv_p, bv_r.x}, {bv_r.yz, packed record, 0} (see pack_node)
     const rt_bvh_node* bvh_src;     // the caller's layout (records that do not pack)
     uint32_t bvh_root_rec;          // the top-level root's packed stack record
+    const float4* top_seq;          // top level in the ray prologue: [8 octants][top_seq_len] x 2 float4, or null
+    uint32_t top_seq_len;
+    uint32_t mlist_max;             // mesh-list capacity, <= MLIST_MAX (RT_MLIST_MAX lowers it for tests)
     uint32_t finite_boxes;          // every node box within 2^40 of the origin (finite_box_ray)
     const uint32_t* bvh_idx;
     const float4* leaf_rec;         // [bvh_index_count][LEAF_REC_Q]: everything a top-level leaf step needs
@@ -324,12 +327,28 @@ constexpr int FETCH_Q = (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u);   // float4 per l
 // traversal would pop first (its box test and the far-clip test against t).  It
 // runs where the ray is made (k_generate / k_shade, all lanes busy), so the trace
 // kernels only see rays that enter the BVH, already carrying t and 1/d.
-struct Prologue { float t; uint32_t code; bool occluded, bvh; V3 inv_d; };
-RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ) {
+//
+// When the top level is small (DevScene::top_seq, built at upload), the prologue
+// also walks it: the top-level BVH as one linear sequence per direction octant in
+// the reference's front-to-back order (:509-517), where a node failing the pop-time
+// test (box hit and tn < t, :107-133) jumps past its subtree.  Spheres and boxes
+// are tested here; a mesh instance whose root box passes goes on the ray's mesh
+// list (bvh_indices slots, 6 bits each, up to MLIST_MAX) and only rays with a
+// non-empty list are queued.  The trace kernel then walks just those instances.
+// Against the reference's interleaved order this only moves analytic tests ahead
+// of mesh traversals: t only decreases and every test keeps its own comparison,
+// so the closest hit is the same unless two surfaces meet at exactly equal t
+// (an any-hit query is order-independent).  More than MLIST_MAX instances: the
+// ray is queued with MLIST_FULL and the kernel re-walks the whole top level
+// (re-testing an analytic primitive at equal t changes nothing: strict tests).
+constexpr uint32_t MLIST_MAX = 4;
+constexpr uint32_t MLIST_FULL = 0xFFFFFFFFu;
+struct Prologue { float t; uint32_t code; bool occluded, bvh; V3 inv_d; uint32_t mlist; };
+RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ, uint32_t ignored) {
     Prologue r;
     Ray wr = make_ray(o, d, max_t);
     wr.zero = 0u;                                                  // no pruning on the world ray
-    r.t = max_t; r.code = RT_HIT_MISS; r.occluded = false; r.bvh = false; r.inv_d = wr.inv_d;
+    r.t = max_t; r.code = RT_HIT_MISS; r.occluded = false; r.bvh = false; r.inv_d = wr.inv_d; r.mlist = MLIST_FULL;
     for (uint32_t i = 0; i < sc.plane_count; ++i) {
         const rt_primitive& pl = sc.planes[i];
         if (ray_plane(wr, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], r.t)) {
@@ -337,12 +356,57 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
             if (occ) { r.occluded = true; return r; }
         }
     }
-    if (sc.bvh_node_count) {
+    if (!sc.bvh_node_count) return r;
+    if (!sc.top_seq) {                                             // large top level: the kernel walks it
         const float4* q = reinterpret_cast<const float4*>(sc.bvh);
         const float4 a = q[0], b = q[1];
         float tn;
         r.bvh = bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn) && tn < r.t;
+        return r;
     }
+    const float4* seq = sc.top_seq + 2*(size_t)sc.top_seq_len*(wr.neg & 7u);
+    uint32_t list = 0, n = 0;
+    bool full = false;
+    for (uint32_t i = 0; i < sc.top_seq_len;) {
+        const float4 a = seq[2*i], b = seq[2*i + 1];
+        float tn;
+        const bool pass = bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn) && tn < r.t;
+        const uint32_t info = __float_as_uint(b.z), skip = __float_as_uint(b.w);
+        if (!pass || !(info >> 31)) { i = pass ? i + 1 : skip; continue; }
+        const uint32_t first = info & 0xFFFFFFu, end = first + ((info >> 24) & 127u);
+        for (uint32_t j = first; j < end; ++j) {                   // the leaf's primitives in order
+            const float4* q = sc.leaf_rec + (size_t)j*LEAF_REC_Q;
+            const float4 q3 = q[3];
+            const uint32_t pi = __float_as_uint(q3.x), type = __float_as_uint(q3.y);
+            if (pi == ignored) continue;
+            M34 inv;
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+            inv.e[0][0] = q0.x; inv.e[0][1] = q0.y; inv.e[0][2] = q0.z; inv.e[0][3] = q0.w;
+            inv.e[1][0] = q1.x; inv.e[1][1] = q1.y; inv.e[1][2] = q1.z; inv.e[1][3] = q1.w;
+            inv.e[2][0] = q2.x; inv.e[2][1] = q2.y; inv.e[2][2] = q2.z; inv.e[2][3] = q2.w;
+            const Ray ir = make_ray(xform(inv, o, 1.0f), xform(inv, d, 0.0f), 0.0f);   // transform_ray :403-409
+            if (type == RT_PRIMITIVE_MESH) {                       // the mesh root's pop-time test (:269-275)
+                const float4 q4 = q[4], q5 = q[5];
+                float tm;
+                if (bv_static(ir, {q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z}, tm) && tm < r.t) {
+                    if (n < sc.mlist_max) list |= j << (6*n);
+                    else full = true;
+                    ++n;
+                }
+                continue;
+            }
+            bool hit = false;
+            if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, q3.z, r.t);
+            else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {q3.z, q3.w, q[4].x}, r.t);
+            if (hit) {
+                r.code = pi;
+                if (occ) { r.occluded = true; return r; }
+            }
+        }
+        i = skip;
+    }
+    r.bvh = n > 0;
+    r.mlist = full ? MLIST_FULL : (list | (n << 24));
     return r;
 }
 
@@ -358,6 +422,9 @@ struct Traversal {
     uint32_t ignored;
     int sp, mode, mesh_base;
     uint32_t leaf_cur, leaf_end;        // TM_LEAF: range of bvh_indices slots still to test
+    uint32_t leaf_list;                 // TM_LEAF from the prologue's mesh list: slots still to walk,
+                                        // 6 bits each (leaf_cur/leaf_end then count the list)
+    bool listed;
     uint32_t inst, node_off, tri_off;   // TM_MESH: the instance
     uint32_t cur_lf, cur_cnt, cur_ax;   // node held by the lane (cur_cnt: leaf size, 0 interior)
     bool has_cur, occluded, finite_world;
@@ -406,7 +473,7 @@ struct Traversal {
         finite_world = false;                                      // debug path: reference max/min chains
         set_world();
         t = max_t; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
-        ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false;
+        ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false; listed = false;
         Ray wr = make_ray(o, d, max_t);
         wr.zero = 0u;                                              // no pruning on the world ray
         for (uint32_t i = 0; i < sc.plane_count; ++i) {            // planes, brute force (:424-433)
@@ -424,15 +491,23 @@ struct Traversal {
         }
     }
 
-    // a queued ray: ray_prologue ran where it was made; it enters the BVH at the root
-    // (whose pop-time test is known to pass: -inf < t)
-    RT_D void init_rec(const DevScene& sc, const Stack& st, V3 o, V3 d, V3 inv_d, float t0, uint32_t ign) {
+    // a queued ray: ray_prologue ran where it was made.  With a mesh list the ray walks
+    // just those instances; with MLIST_FULL it enters the BVH at the root (whose pop-time
+    // test is known to pass: -inf < t)
+    RT_D void init_rec(const DevScene& sc, const Stack& st, V3 o, V3 d, V3 inv_d, float t0, uint32_t ign,
+                       uint32_t mlist) {
         wo = o; wd = d; co = o; cd = d; cinv = inv_d;
         finite_world = sc.finite_boxes && finite_box_ray(o, inv_d);
         cflags = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u) | (finite_world ? 64u : 0u);
         t = t0; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
-        ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false;
-        st.put(sp++, sc.bvh_root_rec, __uint_as_float(0xFF800000u));
+        ignored = ign; sp = 0; occluded = false; has_cur = false;
+        if (mlist == MLIST_FULL) {
+            mode = TM_TOP; listed = false;
+            st.put(sp++, sc.bvh_root_rec, __uint_as_float(0xFF800000u));
+        } else {
+            mode = TM_LEAF; listed = true;
+            leaf_list = mlist & 0xFFFFFFu; leaf_cur = 0; leaf_end = mlist >> 24;
+        }
     }
 
     // pop until an entry above `base` survives the far-clip test (the reference's pop-time
@@ -479,7 +554,7 @@ struct Traversal {
         uint32_t nq;
         if (mode == TM_LEAF) {
             RT_STAT(6);
-            src = sc.leaf_rec + (size_t)leaf_cur*LEAF_REC_Q; nq = LEAF_REC_Q;
+            src = sc.leaf_rec + (size_t)(listed ? (leaf_list & 63u) : leaf_cur)*LEAF_REC_Q; nq = LEAF_REC_Q;
         } else if (cur_cnt) {                                      // mesh leaf
             RT_STAT(5);
             src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
@@ -495,7 +570,7 @@ struct Traversal {
         // 3. arithmetic
         if (mode == TM_LEAF) {
             const uint32_t pi = __float_as_uint(F[3].x);
-            ++leaf_cur;
+            ++leaf_cur; leaf_list >>= 6;
             if (pi == ignored) return true;
             const uint32_t type = __float_as_uint(F[3].y);
             M34 inv;
@@ -1029,7 +1104,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
         cast = st.max_bounce_count > 0;
         pool.state[slot] = cast ? S_TRACE : S_DONE;      // max_bounce_count == 0: nothing to trace
         if (cast) {
-            pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false);
+            pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false, 0u);
             pool.hit[slot] = make_float4(pro.t, __uint_as_float(pro.code), 0.0f, 0.0f);
             pool.hit_w[slot] = 0.0f;
             enqueue = pro.bvh;
@@ -1043,7 +1118,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st,
         float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + pos);
         q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
         q[1] = make_float4(nrd.x, nrd.y, nrd.z, pro.t);
-        q[2] = make_float4(pro.inv_d.x, pro.inv_d.y, pro.inv_d.z, 0.0f);
+        q[2] = make_float4(pro.inv_d.x, pro.inv_d.y, pro.inv_d.z, __uint_as_float(pro.mlist));
     }
 }
 
@@ -1144,7 +1219,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                 const float4* q = (OCC ? pool.sh_rec : pool.ext_rec[cur]) + REC_Q*(size_t)item;
                 const float4 o = q[0], d = q[1], iv = q[2];
                 if (!OCC) item = __float_as_uint(o.w);            // the path's slot
-                tr.init_rec(sc, st, ld3(o), ld3(d), ld3(iv), d.w, OCC ? __float_as_uint(o.w) : 0u);
+                tr.init_rec(sc, st, ld3(o), ld3(d), ld3(iv), d.w, OCC ? __float_as_uint(o.w) : 0u, __float_as_uint(iv.w));
                 steps = 0;
                 if (tr.mode == TM_DONE) finish(); else active = true;
             }
@@ -1303,7 +1378,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
                                 cast_shadow = true;
                                 // intersect_shadow_ray (:756): planes and the root here; only rays
                                 // that enter the BVH are queued for k_trace<true>
-                                spro = ray_prologue(sc, sh_o, sh_d, sh_t, true);
+                                spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, lid);
                                 shadow = !spro.occluded && spro.bvh;
                                 if (!spro.occluded && !spro.bvh) total = add(total, sh_c);   // :768
                             }
@@ -1340,7 +1415,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
         cont = !done;
         nro = ro; nrd = rd;
         if (cont) {                                        // next bounce's intersect_scene: planes + root here
-            cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false);
+            cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
             pool.hit[slot] = make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f);
             pool.hit_w[slot] = 0.0f;
             enq = cpro.bvh;
@@ -1361,7 +1436,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
         float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + pos);
         q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
         q[1] = make_float4(nrd.x, nrd.y, nrd.z, cpro.t);
-        q[2] = make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, 0.0f);
+        q[2] = make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, __uint_as_float(cpro.mlist));
     }
     uint32_t spos = shard*pool.shard_cap + block_append<BLOCK>(&cnt->shadow_count[shard][0], shadow, agg);
     if (shadow) {
@@ -1369,7 +1444,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
         float4* q = pool.sh_rec + REC_Q*(size_t)spos;
         q[0] = make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light));
         q[1] = make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t);
-        q[2] = make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, 0.0f);
+        q[2] = make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist));
         pool.sh_c[spos] = make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f);
     }
     if (done) pool.state[slot] = S_DONE;
@@ -1652,20 +1727,35 @@ __global__ void __launch_bounds__(256) k_post(const float4* px, uint32_t w, uint
 // ======================================================================
 // Host side: rt_scene + C ABI
 // ======================================================================
+// A partition: one independent wavefront loop (its own path pool, queues,
+// counters and traversal spill area) on its own stream.  run_frame splits the
+// frame's samples between RT_PARTITIONS of them and interleaves their launches,
+// so one partition's kernels fill the GPU while another's persistent trace
+// kernel drains its last long rays (the per-launch tail).
+constexpr int MAX_PARTITIONS = 8;
+struct Partition {
+    Pool pool = {};
+    std::vector<void*> pool_allocs;
+    Counters* cnt = nullptr;
+    Counters* cnt_host = nullptr;       // pinned
+    uint2* spill = nullptr;             // traversal stack levels beyond STACK_LDS
+    hipStream_t own_stream = nullptr;   // partitions > 0 (partition 0 runs on the caller's stream)
+    hipEvent_t join = nullptr;
+    hipEvent_t ev[EV_SLOTS * 2 * RT_KERNEL_COUNT] = {};
+    bool events = false;
+};
+
 struct rt_scene {
     int device = 0;
     DevScene ds = {};
     std::vector<void*> allocs;
     // render-time state (grown on demand)
-    Pool pool = {};
-    std::vector<void*> pool_allocs;
-    Counters* cnt = nullptr;
-    Counters* cnt_host = nullptr;       // pinned
+    Partition part[MAX_PARTITIONS];
+    hipEvent_t start_ev = nullptr;
     uint32_t* d_tiles = nullptr;
     size_t tiles_cap = 0;
     int32_t* d_tile_base = nullptr;
     size_t tile_base_cap = 0;
-    uint2* d_spill = nullptr;       // traversal stack levels beyond STACK_LDS
     uint32_t trace_grid = 0;        // persistent k_trace blocks
     float4* d_samp = nullptr;       // per-sample records for the deterministic splat
     float* d_samp_jy = nullptr;
@@ -1673,8 +1763,6 @@ struct rt_scene {
     float* d_lut = nullptr;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
-    hipEvent_t ev[EV_SLOTS * 2 * RT_KERNEL_COUNT] = {};
-    bool events = false;
 };
 
 namespace {
@@ -1704,6 +1792,45 @@ std::vector<rt_bvh_node> traversal_layout(const rt_bvh_node* nodes, uint32_t cou
     return out;
 }
 
+// The top level for ray_prologue: for each direction octant, the nodes in the
+// reference's visit order (children by d_is_negative[split_axis], RT/intersection.cpp:
+// 509-517) as {bv_p, bv_r.x}, {bv_r.yz, info, skip}: info = 0x80000000 | count << 24 |
+// first for a leaf, 0 for an interior node; skip = the entry after the node's subtree.
+// Empty when the top level is too large for the prologue's 6-bit mesh list.
+std::vector<float4> top_sequences(const rt_bvh_node* nodes, uint32_t count, uint32_t index_count, uint32_t& len) {
+    len = 0;
+    if (!count || count > 255 || index_count > 63) return {};
+    auto u2f = [](uint32_t u) { float f; memcpy(&f, &u, 4); return f; };
+    std::vector<float4> out;
+    for (uint32_t oct = 0; oct < 8; ++oct) {
+        std::vector<float4> seq;
+        bool ok = true;
+        auto emit = [&](auto&& self, uint32_t n, uint32_t depth) -> void {
+            if (!ok || n >= count || depth > 64) { ok = false; return; }
+            const rt_bvh_node& nd = nodes[n];
+            const size_t at = seq.size();
+            seq.push_back(make_float4(nd.bv_p.x, nd.bv_p.y, nd.bv_p.z, nd.bv_r.x));
+            seq.push_back(make_float4(nd.bv_r.y, nd.bv_r.z, 0.0f, 0.0f));
+            if (nd.count) {
+                if (nd.count > 127 || nd.left_first + nd.count > index_count) { ok = false; return; }
+                seq[at + 1].z = u2f(0x80000000u | (nd.count << 24) | nd.left_first);
+            } else if (nd.left_first == 0 || nd.left_first + 1 >= count || nd.split_axis > 2) {
+                seq[at + 1].z = u2f(0x80000000u);                 // nothing below: an empty leaf
+            } else {
+                const bool neg = (oct >> nd.split_axis) & 1u;     // right child first when d < 0
+                self(self, nd.left_first + (neg ? 1u : 0u), depth + 1);
+                self(self, nd.left_first + (neg ? 0u : 1u), depth + 1);
+            }
+            seq[at + 1].w = u2f((uint32_t)(seq.size() / 2));
+        };
+        emit(emit, 0u, 0u);
+        if (!ok) return {};
+        len = (uint32_t)(seq.size() / 2);
+        out.insert(out.end(), seq.begin(), seq.end());
+    }
+    return out;
+}
+
 uint32_t tree_depth(const rt_bvh_node* nodes, uint32_t count) {
     if (!count) return 0;
     uint32_t maxd = 0;
@@ -1722,19 +1849,42 @@ uint32_t tree_depth(const rt_bvh_node* nodes, uint32_t count) {
     return maxd;
 }
 
-void free_pool(rt_scene* s) {
-    for (void* p : s->pool_allocs) (void)hipFree(p);
-    s->pool_allocs.clear();
-    s->pool = Pool{};
+void free_pool(Partition& pt) {
+    for (void* p : pt.pool_allocs) (void)hipFree(p);
+    pt.pool_allocs.clear();
+    pt.pool = Pool{};
 }
 
-int ensure_pool(rt_scene* s, uint32_t n) {
-    if (s->pool.n >= n) return RT_OK;
-    free_pool(s);
-    Pool& p = s->pool;
+void free_partition(Partition& pt) {
+    free_pool(pt);
+    if (pt.cnt) (void)hipFree(pt.cnt);
+    if (pt.cnt_host) (void)hipHostFree(pt.cnt_host);
+    if (pt.spill) (void)hipFree(pt.spill);
+    if (pt.own_stream) (void)hipStreamDestroy(pt.own_stream);
+    if (pt.join) (void)hipEventDestroy(pt.join);
+    if (pt.events) for (auto& e : pt.ev) (void)hipEventDestroy(e);
+    pt = Partition{};
+}
+
+// counters, spill area, stream and events of partition k (allocated on first use)
+int ensure_partition(rt_scene* s, int k) {
+    Partition& pt = s->part[k];
+    if (pt.cnt) return RT_OK;
+    HIP_OK(hipMalloc(&pt.cnt, sizeof(Counters)));
+    HIP_OK(hipHostMalloc(&pt.cnt_host, sizeof(Counters)));
+    HIP_OK(hipMalloc(&pt.spill, sizeof(uint2)*(size_t)(STACK_DEPTH - STACK_LDS)*s->trace_grid*TB));
+    if (k > 0) HIP_OK(hipStreamCreateWithFlags(&pt.own_stream, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&pt.join, hipEventDisableTiming));
+    return RT_OK;
+}
+
+int ensure_pool(Partition& pt, uint32_t n) {
+    if (pt.pool.n >= n) return RT_OK;
+    free_pool(pt);
+    Pool& p = pt.pool;
     auto alloc = [&](void** ptr, size_t bytes) -> int {
         HIP_OK(hipMalloc(ptr, bytes));
-        s->pool_allocs.push_back(*ptr);
+        pt.pool_allocs.push_back(*ptr);
         return RT_OK;
     };
     int e = 0;
@@ -1761,7 +1911,7 @@ int ensure_pool(rt_scene* s, uint32_t n) {
     e |= alloc((void**)&p.sh_slot, 4*Q);
     e |= alloc((void**)&p.sh_rec, 16*REC_Q*Q);
     e |= alloc((void**)&p.sh_c, 16*Q);
-    if (e) { free_pool(s); return RT_ERROR_OUT_OF_MEMORY; }
+    if (e) { free_pool(pt); return RT_ERROR_OUT_OF_MEMORY; }
     p.n = n;
     return RT_OK;
 }
@@ -1777,88 +1927,137 @@ int check_inputs(const rt_settings* st, const rt_filter_cache* f) {
 }
 
 // The wavefront driver shared by rt_render_device and rt_trace_samples.
+// The frame's samples [0, total) are split into contiguous ranges, one per
+// partition (RT_PARTITIONS, default 4); each partition runs generate -> extend ->
+// shade -> connect -> splat -> bookkeep on its own stream, and the host enqueues
+// the partitions' iterations interleaved.  Results do not depend on the split:
+// every sample is keyed by its own number (the RNG seed and the record slot).
 int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long long total, hipStream_t stream, rt_stats* stats) {
     auto t0 = std::chrono::steady_clock::now();
+    int nparts = 4;
+    if (const char* e = getenv("RT_PARTITIONS")) nparts = std::max(1, std::min(MAX_PARTITIONS, atoi(e)));
     uint32_t pool_n = g_pool_override ? g_pool_override : (1u << 21);
+    // small frames: one partition, pool no larger than the work
+    if ((unsigned long long)pool_n*nparts > total) nparts = 1;
     if ((unsigned long long)pool_n > total) pool_n = (uint32_t)std::max<unsigned long long>(total, 1ull);
     pool_n = (pool_n + BLOCK - 1) / BLOCK * BLOCK;
-    int err = ensure_pool(s, pool_n);
-    if (err) return err;
-    Pool pool = s->pool;
-    const uint32_t N = pool.n;
-    Counters init = {};
-    init.total_samples = total;
-    HIP_OK(hipMemcpyAsync(s->cnt, &init, sizeof(Counters), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemsetAsync(pool.state, S_FREE, N, stream));
-    const uint32_t grid = (N + BLOCK - 1) / BLOCK;
-    HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pool.free_n, BLOCK, grid, stream));   // N is a multiple of BLOCK
-    k_bookkeep<<<1, BK_THREADS, 0, stream>>>(s->cnt, pool, grid, 0, 1);
+    const bool prof = g_profiling;
+    const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
+    if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(s->start_ev, stream));
+    struct Run { hipStream_t stream; uint32_t grid; uint64_t iters; int cur; bool live; int pending[EV_SLOTS]; int npending; };
+    Run run[MAX_PARTITIONS] = {};
     double kms[RT_KERNEL_COUNT] = {};
     uint64_t klaunch[RT_KERNEL_COUNT] = {};
-    const bool prof = g_profiling;
-    if (prof && !s->events) {
-        for (auto& e : s->ev) HIP_OK(hipEventCreate(&e));
-        s->events = true;
+    for (int k = 0; k < nparts; ++k) {
+        int err = ensure_partition(s, k);
+        if (!err) err = ensure_pool(s->part[k], pool_n);
+        if (err) return err;
+        Partition& pt = s->part[k];
+        Run& r = run[k];
+        r.stream = k ? pt.own_stream : stream;
+        if (k) HIP_OK(hipStreamWaitEvent(r.stream, s->start_ev, 0));   // the caller's prior work (buffers, tables)
+        const uint32_t N = pt.pool.n;
+        r.grid = (N + BLOCK - 1) / BLOCK;
+        r.live = true;
+        Counters init = {};
+        init.next_sample = total*(unsigned long long)k / nparts;
+        init.total_samples = total*(unsigned long long)(k + 1) / nparts;
+        HIP_OK(hipMemcpyAsync(pt.cnt, &init, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
+        HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
+        HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
+        k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, 0, 1);
+        if (prof && !pt.events) {
+            for (auto& e : pt.ev) HIP_OK(hipEventCreate(&e));
+            pt.events = true;
+        }
     }
     // Stage timing without extra host syncs: each iteration records begin/end
     // events into one of EV_SLOTS ring slots; the slots are read back at the
     // host sync points the loop already has (every 4 iterations).
-    int pending[EV_SLOTS];
-    int npending = 0;
-    auto ev = [&](int slot, int k, int end) -> hipEvent_t& { return s->ev[(slot*RT_KERNEL_COUNT + k)*2 + end]; };
-    auto stage_begin = [&](int slot, int k) { if (prof) (void)hipEventRecord(ev(slot, k, 0), stream); };
-    auto stage_end = [&](int slot, int k) { if (prof) (void)hipEventRecord(ev(slot, k, 1), stream); };
-    auto harvest = [&]() {
-        for (int i = 0; i < npending; ++i)
-            for (int k = 0; k < RT_KERNEL_COUNT - 1; ++k) {
+    auto ev = [&](int k, int slot, int kern, int end) -> hipEvent_t& {
+        return s->part[k].ev[(slot*RT_KERNEL_COUNT + kern)*2 + end];
+    };
+    auto harvest = [&](int k) {
+        Run& r = run[k];
+        for (int i = 0; i < r.npending; ++i)
+            for (int kern = 0; kern < RT_KERNEL_COUNT - 1; ++kern) {
                 float ms = 0.0f;
-                if (hipEventElapsedTime(&ms, ev(pending[i], k, 0), ev(pending[i], k, 1)) == hipSuccess) {
-                    kms[k] += ms; klaunch[k] += 1;
+                if (hipEventElapsedTime(&ms, ev(k, r.pending[i], kern, 0), ev(k, r.pending[i], kern, 1)) == hipSuccess) {
+                    kms[kern] += ms; klaunch[kern] += 1;
                 }
             }
-        npending = 0;
+        r.npending = 0;
+    };
+    auto iterate = [&](int k) {
+        Partition& pt = s->part[k];
+        Run& r = run[k];
+        const hipStream_t q = r.stream;
+        const int slot = (int)(r.iters % EV_SLOTS);
+        if (prof) r.pending[r.npending++] = slot;
+        auto b = [&](int kern) { if (prof) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
+        auto e = [&](int kern) { if (prof) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
+        b(RT_KERNEL_GENERATE);
+        k_generate<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
+        k_trace<false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
+        k_shade<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
+        k_trace<true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        e(RT_KERNEL_CONNECT); b(RT_KERNEL_SPLAT);
+        k_splat<<<r.grid, BLOCK, 0, q>>>(fp, pt.pool, pt.cnt);
+        e(RT_KERNEL_SPLAT);
+        k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pt.pool, r.grid, r.cur, 0);
+        ++r.iters;
+        r.cur ^= 1;
     };
     s->cancel = 0;
-    const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
-    uint64_t iters = 0;
-    int cur = 0;
-    for (;;) {
-        const int slot = (int)(iters % EV_SLOTS);
-        if (prof) pending[npending++] = slot;
-        stage_begin(slot, RT_KERNEL_GENERATE);
-        k_generate<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
-        stage_end(slot, RT_KERNEL_GENERATE);
-        stage_begin(slot, RT_KERNEL_EXTEND);
-        k_trace<false><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill, diag);
-        stage_end(slot, RT_KERNEL_EXTEND);
-        stage_begin(slot, RT_KERNEL_SHADE);
-        k_shade<<<grid, BLOCK, 0, stream>>>(s->ds, *st, fp, pool, s->cnt, cur);
-        stage_end(slot, RT_KERNEL_SHADE);
-        stage_begin(slot, RT_KERNEL_CONNECT);
-        k_trace<true><<<s->trace_grid, TB, 0, stream>>>(s->ds, pool, s->cnt, cur, s->d_spill, diag);
-        stage_end(slot, RT_KERNEL_CONNECT);
-        stage_begin(slot, RT_KERNEL_SPLAT);
-        k_splat<<<grid, BLOCK, 0, stream>>>(fp, pool, s->cnt);
-        stage_end(slot, RT_KERNEL_SPLAT);
-        k_bookkeep<<<1, BK_THREADS, 0, stream>>>(s->cnt, pool, grid, cur, 0);
+    uint64_t rounds = 0;
+    for (int live = nparts; live > 0; ++rounds) {
+        // a round: 4 iterations of every live partition, interleaved (1 in the first 3 rounds),
+        // then each partition's counters come back for the termination test
+        const int per_round = rounds < 3 ? 1 : 4;
+        for (int i = 0; i < per_round; ++i)
+            for (int k = 0; k < nparts; ++k)
+                if (run[k].live) iterate(k);
         HIP_OK(hipGetLastError());
-        ++iters;
-        cur ^= 1;
-        if ((iters & 3u) == 0u || iters < 4) {
-            HIP_OK(hipMemcpyAsync(s->cnt_host, s->cnt, sizeof(Counters), hipMemcpyDeviceToHost, stream));
-            HIP_OK(hipStreamSynchronize(stream));
-            harvest();
-            const Counters& c = *s->cnt_host;
-            if (c.next_sample >= c.total_samples && c.pending == 0) break;
-            if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
-            if (iters > 100000) { set_error("wavefront loop did not converge"); return RT_ERROR_DEVICE; }
+        for (int k = 0; k < nparts; ++k)
+            if (run[k].live)
+                HIP_OK(hipMemcpyAsync(s->part[k].cnt_host, s->part[k].cnt, sizeof(Counters), hipMemcpyDeviceToHost, run[k].stream));
+        for (int k = 0; k < nparts; ++k) {
+            if (!run[k].live) continue;
+            HIP_OK(hipStreamSynchronize(run[k].stream));
+            harvest(k);
+            const Counters& c = *s->part[k].cnt_host;
+            if (c.next_sample >= c.total_samples && c.pending == 0) { run[k].live = false; --live; }
         }
+        if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
+        if (rounds > 100000) { set_error("wavefront loop did not converge"); return RT_ERROR_DEVICE; }
     }
-    HIP_OK(hipMemcpyAsync(s->cnt_host, s->cnt, sizeof(Counters), hipMemcpyDeviceToHost, stream));
-    HIP_OK(hipStreamSynchronize(stream));
-    harvest();
-    if (getenv("RT_DEBUG_TRAVERSAL")) {
-        const Counters& c = *s->cnt_host;
+    for (int k = 1; k < nparts; ++k) {                     // the caller's stream continues after every partition
+        HIP_OK(hipEventRecord(s->part[k].join, run[k].stream));
+        HIP_OK(hipStreamWaitEvent(stream, s->part[k].join, 0));
+    }
+    Counters sum = {};
+    uint64_t iters = 0;
+    for (int k = 0; k < nparts; ++k) {
+        const Counters& c = *s->part[k].cnt_host;
+        sum.closest_rays += c.closest_rays;
+        sum.shadow_rays += c.shadow_rays;
+        sum.traced_rays[0] += c.traced_rays[0];
+        sum.traced_rays[1] += c.traced_rays[1];
+        for (int a = 0; a < 2; ++a) {
+            for (int i = 0; i < 8; ++i) sum.step_stats[a][i] += c.step_stats[a][i];
+            if (c.max_steps[a] >= sum.max_steps[a]) {
+                sum.max_steps[a] = c.max_steps[a];
+                memcpy(sum.worst_ray[a], c.worst_ray[a], sizeof(sum.worst_ray[a]));
+            }
+        }
+        iters = std::max(iters, run[k].iters);
+    }
+    if (diag) {
+        const Counters& c = sum;
         for (int k = 0; k < 2; ++k) {
             const unsigned long long* v = c.step_stats[k];
             if (!v[1]) continue;
@@ -1874,14 +2073,14 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     }
     if (stats) {
         memset(stats, 0, sizeof(*stats));
-        stats->closest_hit_rays = s->cnt_host->closest_rays;
-        stats->shadow_rays = s->cnt_host->shadow_rays;
+        stats->closest_hit_rays = sum.closest_rays;
+        stats->shadow_rays = sum.shadow_rays;
         stats->samples = total;
         stats->iterations = iters;
         stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int k = 0; k < RT_KERNEL_COUNT; ++k) { stats->kernel_ms[k] = kms[k]; stats->kernel_launches[k] = klaunch[k]; }
-        stats->traced_rays[0] = s->cnt_host->traced_rays[0];
-        stats->traced_rays[1] = s->cnt_host->traced_rays[1];
+        stats->traced_rays[0] = sum.traced_rays[0];
+        stats->traced_rays[1] = sum.traced_rays[1];
     }
     return RT_OK;
 }
@@ -1980,6 +2179,18 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         if ((err = upload(s, tl.data(), tl.size(), &ds.bvh))) return fail(err);
     }
     if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
+    {
+        const char* env = getenv("RT_TOP_PROLOGUE");              // 0: the trace kernels walk the top level
+        std::vector<float4> seq;
+        uint32_t len = 0;
+        if (!(env && env[0] == '0')) seq = top_sequences(d->bvh_nodes, d->bvh_node_count, d->bvh_index_count, len);
+        ds.top_seq = nullptr; ds.top_seq_len = 0; ds.mlist_max = MLIST_MAX;
+        if (const char* m = getenv("RT_MLIST_MAX")) ds.mlist_max = std::min<uint32_t>(MLIST_MAX, (uint32_t)atoi(m));
+        if (!seq.empty()) {
+            if ((err = upload(s, seq.data(), seq.size(), &ds.top_seq))) return fail(err);
+            ds.top_seq_len = len;
+        }
+    }
     ds.bvh_node_count = d->bvh_node_count;
     // meshes: concatenate, triangles as (a, b-a, c-a) float4 triples
     std::vector<DevMesh> meshes(d->mesh_count);
@@ -2087,11 +2298,8 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
-        const size_t spill_bytes = sizeof(uint2)*(size_t)(STACK_DEPTH - STACK_LDS)*s->trace_grid*TB;
-        if (hipMalloc(&s->d_spill, spill_bytes) != hipSuccess) { set_error("hipMalloc spill"); return fail(RT_ERROR_OUT_OF_MEMORY); }
     }
-    if (hipMalloc(&s->cnt, sizeof(Counters)) != hipSuccess) { set_error("hipMalloc counters"); return fail(RT_ERROR_OUT_OF_MEMORY); }
-    if (hipHostMalloc(&s->cnt_host, sizeof(Counters)) != hipSuccess) { set_error("hipHostMalloc"); return fail(RT_ERROR_OUT_OF_MEMORY); }
+    if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
     *out = s;
     return RT_OK;
@@ -2101,16 +2309,13 @@ int rt_scene_free(rt_scene* s) {
     if (!s) return RT_OK;
     (void)hipSetDevice(s->device);
     for (void* p : s->allocs) (void)hipFree(p);
-    free_pool(s);
-    if (s->cnt) (void)hipFree(s->cnt);
-    if (s->cnt_host) (void)hipHostFree(s->cnt_host);
+    for (auto& pt : s->part) free_partition(pt);
+    if (s->start_ev) (void)hipEventDestroy(s->start_ev);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
     if (s->d_tile_base) (void)hipFree(s->d_tile_base);
-    if (s->d_spill) (void)hipFree(s->d_spill);
     if (s->d_samp) (void)hipFree(s->d_samp);
     if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
     if (s->d_lut) (void)hipFree(s->d_lut);
-    if (s->events) for (auto& e : s->ev) (void)hipEventDestroy(e);
     delete s;
     return RT_OK;
 }

@@ -271,3 +271,27 @@ def test_postprocess_bit_exact(c1, frame):
         same.append(float((gpu == cpu).mean()))
         assert np.array_equal(gpu, cpu), f"{(gpu != cpu).sum()} pixels differ"
     REPORT[f"postprocess_frame{frame}"] = {"pixels_bit_identical": same}
+
+
+@pytest.mark.parametrize("env", [{"RT_TOP_PROLOGUE": "0"}, {"RT_MLIST_MAX": "1"}, {"RT_MLIST_MAX": "0"}])
+def test_top_level_paths(rt, env, monkeypatch):
+    """The three ways a queued ray meets the top level (ray prologue):
+    the trace kernel walks all of it (RT_TOP_PROLOGUE=0), the prologue tests the
+    analytic primitives and the kernel re-walks everything because the mesh list
+    overflowed (RT_MLIST_MAX=1 on C4's four instances, and 0), or the default mesh
+    list (the other tests).  Per-sample results stay bit-exact against the oracle."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    scene, cam, st, fc, post = rt.load_preset("c4", 192, 108)
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        rng = np.random.default_rng(5)
+        xy, s = _sample_list(rng, 192, 108, 20000, st.samples_per_pixel)
+        gpu, gstats = dev.trace_samples(cam, st, 192, 108, xy, s)
+    finally:
+        dev.close()
+    cpu, cstats = ob.trace_samples(scene.desc(), cam, st, 192, 108, xy, s)
+    same = np.all((gpu == cpu) | (np.isnan(gpu) & np.isnan(cpu)), axis=1).mean()
+    REPORT["top_level_" + "_".join(f"{k}={v}" for k, v in env.items())] = {"bit_exact_fraction": float(same)}
+    assert same >= 0.999
+    assert gstats.closest_hit_rays == cstats.closest_hit_rays or same < 1.0
