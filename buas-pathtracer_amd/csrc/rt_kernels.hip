@@ -1515,22 +1515,38 @@ __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Coun
 // (try_render_next_tile, :555), pixels in raster order inside a tile, samples
 // in order (render_tile, :409-422).  The float additions are therefore the
 // reference's, bit for bit, and need no atomics.
-constexpr int RES_TILE = 16;
-__global__ void __launch_bounds__(RES_TILE*RES_TILE) k_resolve(FrameParams fp) {
+//
+// A thread owns a column strip of RES_RY output pixels.  Every pixel's order is
+// the one global order restricted to its (2r+1)^2 window, so the thread walks
+// the union of its pixels' windows once in that order and adds each sample
+// record to every pixel of the strip whose window holds it: a record is read
+// once per strip instead of once per pixel ((RES_RY + 2r)(2r+1) reads for
+// RES_RY pixels, 60 instead of 200 at r = 2).  The 64 lanes of a wave own 64
+// adjacent columns, so at every step they read 64 adjacent records of one
+// sample plane (record = s*P + p): the loads stay coalesced.
+#ifndef RT_RES_RY
+#define RT_RES_RY 8
+#endif
+constexpr int RES_RY = RT_RES_RY;
+constexpr int RES_BX = 64, RES_BY = 4;
+__global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
     __shared__ float lut[512];
-    for (int i = threadIdx.x; i < 512; i += RES_TILE*RES_TILE) lut[i] = fp.cache_size ? fp.lut[i] : 0.0f;
+    for (int i = threadIdx.x; i < 512; i += RES_BX*RES_BY) lut[i] = fp.cache_size ? fp.lut[i] : 0.0f;
     __syncthreads();
-    const int X = blockIdx.x*RES_TILE + (threadIdx.x % RES_TILE);
-    const int Y = blockIdx.y*RES_TILE + (threadIdx.x / RES_TILE);
+    const int X = blockIdx.x*RES_BX + (threadIdx.x % RES_BX);
+    const int Y0 = (blockIdx.y*RES_BY + (threadIdx.x / RES_BX))*RES_RY;
     const int W = (int)fp.w, H = (int)fp.h;
-    if (X >= W || Y >= H) return;
+    if (X >= W || Y0 >= H) return;
     const int ks = fp.cache_size ? fp.kernel_size : 0;
     const float kscale = ks ? (float)(fp.cache_size - 1) / (float)ks : 0.0f;
     const int TW = (int)fp.tile_w, TH = (int)fp.tile_h;
     const int x0 = max(X - ks, 0), x1 = min(X + ks, W - 1);
-    const int y0 = max(Y - ks, 0), y1 = min(Y + ks, H - 1);
-    float4 acc = fp.accum[(size_t)Y*W + X];
+    const int y0 = max(Y0 - ks, 0), y1 = min(Y0 + RES_RY - 1 + ks, H - 1);
+    float4 acc[RES_RY];
+#pragma unroll
+    for (int r = 0; r < RES_RY; ++r) acc[r] = (Y0 + r < H) ? fp.accum[(size_t)(Y0 + r)*W + X] : make_float4(0, 0, 0, 0);
     const size_t P = fp.pixels;
+    const float dx = (float)(X);
     for (int ty = y1 / TH; ty >= y0 / TH; --ty) {
         for (int tx = x1 / TW; tx >= x0 / TW; --tx) {
             const int tile = ty*(int)fp.tcx + tx;
@@ -1541,33 +1557,49 @@ __global__ void __launch_bounds__(RES_TILE*RES_TILE) k_resolve(FrameParams fp) {
             const int ya = max(y0, min_y), yb = min(y1, min_y + TH - 1);
             const int xa = max(x0, min_x), xb = min(x1, min_x + TW - 1);
             for (int y = ya; y <= yb; ++y) {
+                // strip pixels whose window holds row y: Y0 + r in [y - ks, y + ks]
+                const int rlo = max(y - ks - Y0, 0), rhi = min(y + ks - Y0, RES_RY - 1);
                 for (int x = xa; x <= xb; ++x) {
                     const size_t p = (size_t)base + (size_t)(y - min_y)*twid + (size_t)(x - min_x);
                     if (ks) {
-                        const float dx = (float)(X - x), dy = (float)(Y - y);
+                        const float fdx = dx - (float)x;
                         for (uint32_t s = 0; s < fp.spp; ++s) {
-                            const size_t r = (size_t)s*P + p;
-                            const float4 c = fp.samp_rgbx[r];
-                            const float jy = fp.samp_jy[r];
-                            const float fx = lut[(int)fabsf(0.5f + kscale*(dx - c.w))];
-                            const float fy = lut[(int)fabsf(0.5f + kscale*(dy - jy))];
-                            const float f = fx*fy;
-                            acc.x = acc.x + f*c.x;
-                            acc.y = acc.y + f*c.y;
-                            acc.z = acc.z + f*c.z;
-                            acc.w = acc.w + f;
+                            const size_t rr = (size_t)s*P + p;
+                            const float4 c = fp.samp_rgbx[rr];
+                            const float jy = fp.samp_jy[rr];
+                            const float fx = lut[(int)fabsf(0.5f + kscale*(fdx - c.w))];
+#pragma unroll
+                            for (int r = 0; r < RES_RY; ++r) {
+                                if (r < rlo || r > rhi) continue;
+                                const float dy = (float)(Y0 + r - y);
+                                const float fy = lut[(int)fabsf(0.5f + kscale*(dy - jy))];
+                                const float f = fx*fy;
+                                acc[r].x = acc[r].x + f*c.x;
+                                acc[r].y = acc[r].y + f*c.y;
+                                acc[r].z = acc[r].z + f*c.z;
+                                acc[r].w = acc[r].w + f;
+                            }
                         }
-                    } else {                                   // box filter: column += (result, 1)
+                    } else {                                   // box filter: the pixel's own samples, (result, 1)
+                        const int r = y - Y0;
+                        if (r < 0 || r >= RES_RY || x != X) continue;
                         for (uint32_t s = 0; s < fp.spp; ++s) {
                             const float4 c = fp.samp_rgbx[(size_t)s*P + p];
-                            acc.x = acc.x + c.x; acc.y = acc.y + c.y; acc.z = acc.z + c.z; acc.w = acc.w + 1.0f;
+#pragma unroll
+                            for (int q = 0; q < RES_RY; ++q)
+                                if (q == r) {
+                                    acc[q].x = acc[q].x + c.x; acc[q].y = acc[q].y + c.y;
+                                    acc[q].z = acc[q].z + c.z; acc[q].w = acc[q].w + 1.0f;
+                                }
                         }
                     }
                 }
             }
         }
     }
-    fp.accum[(size_t)Y*W + X] = acc;
+#pragma unroll
+    for (int r = 0; r < RES_RY; ++r)
+        if (Y0 + r < H) fp.accum[(size_t)(Y0 + r)*W + X] = acc[r];
 }
 
 // k_bookkeep — end of iteration (one workgroup): ray counts, counter roll-over,
@@ -2451,8 +2483,8 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     auto t0 = std::chrono::steady_clock::now();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_profiling) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
-    dim3 rgrid((w + RES_TILE - 1) / RES_TILE, (h + RES_TILE - 1) / RES_TILE);
-    k_resolve<<<rgrid, RES_TILE*RES_TILE, 0, stream>>>(fp);
+    dim3 rgrid((w + RES_BX - 1) / RES_BX, (h + RES_BY*RES_RY - 1) / (RES_BY*RES_RY));
+    k_resolve<<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
     HIP_OK(hipGetLastError());
     if (g_profiling) HIP_OK(hipEventRecord(e1, stream));
     HIP_OK(hipStreamSynchronize(stream));
