@@ -14,12 +14,17 @@ are split over the ranks.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (k_extend,
-the closest-hit traversal): algorithmic bytes = 48 B per traced ray (read ray
-32 B + write hit 16 B) x rays per launch / mean launch time,
-measured with HIP events on the render stream.  `cpu_baseline` is the CPU
-restatement (oracle/, reference-stream RNG, 64x64 tile queue) timed on this
-box's cores over a bounded sample of the same workload.
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel: the stage
+with the most GPU time in the timed region (k_shade on C3), algorithmic bytes =
+its SURVEY.md §8(d) bytes per unit (BYTES_PER_UNIT) x units per launch / mean
+launch time, measured with HIP events on the stream of the partition that
+launched it.  Four partitions run concurrently, so the launch
+time includes shared GPU time: `concurrency` gives the mean number of kernels in
+flight, `isolated` the serialized figures from the rocprofv3 --pmc runs, and
+`pipeline` the whole-frame figure of SURVEY.md §8(d) (152 B per ray + 144 B per
+sample over wall time).  `cpu_baseline` is the CPU restatement (oracle/,
+reference-stream RNG, 64x64 tile queue) timed on this box's cores over a
+bounded sample of the same workload.
 """
 import argparse
 import ctypes as C
@@ -32,9 +37,18 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table
-# k_extend algorithmic bytes per traced ray: the queued record (o|slot, d|t, 1/d: 48 B) in,
-# the hit record (t, primitive, triangle, v, w: 20 B) out
-EXTEND_BYTES_PER_RAY = 68
+STAGES = ["generate", "extend", "shade", "connect", "splat", "resolve"]
+KERNEL = {"generate": "k_generate", "extend": "k_extend", "shade": "k_shade", "connect": "k_connect",
+          "splat": "k_splat", "resolve": "k_resolve"}
+# Algorithmic HBM bytes per unit of work, with the unit each launch processes:
+#   generate: a new path's ray (32 B) + path state (48 B) written                  per sample
+#   extend:   the queued record (o|slot, d|t, 1/d: 48 B) in, the hit (20 B) out    per traced closest-hit ray
+#   shade:    hit 16 + state 48 in, state 48 + next ray 32 + shadow ray 48 out    per closest-hit query shaded
+#   connect:  the shadow record (48 B) + contribution (16 B) in                   per traced shadow ray
+#   splat:    path state 48 B in, the 16 B sample record out                      per sample
+BYTES_PER_UNIT = {"generate": 80, "extend": 68, "shade": 192, "connect": 64, "splat": 64}
+# whole-pipeline figure of SURVEY.md §8(d): B_alg = 152 B per ray + 144 B per sample
+PIPE_BYTES_PER_RAY, PIPE_BYTES_PER_SAMPLE = 152, 144
 CONFIGS = {
     "c1": dict(preset="c1", w=512, h=512),
     "c2": dict(preset="c2", w=1920, h=1080),
@@ -163,7 +177,7 @@ def main():
     torch.cuda.synchronize(device)
 
     rt.lib().rt_set_profiling(1)
-    closest = shadow = samples = traced = 0
+    closest = shadow = samples = traced = traced_sh = 0
     kms = [0.0] * 6
     kl = [0] * 6
     if distributed:
@@ -176,6 +190,7 @@ def main():
         shadow += s.shadow_rays
         samples += s.samples
         traced += s.traced_rays[0]
+        traced_sh += s.traced_rays[1]
         for k in range(6):
             kms[k] += s.kernel_ms[k]
             kl[k] += s.kernel_launches[k]
@@ -187,30 +202,43 @@ def main():
 
     totals = torch.tensor([closest, shadow, samples], dtype=torch.float64, device=f"cuda:{device}")
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
-    ext = torch.tensor([kms[1], kl[1], traced], dtype=torch.float64, device=f"cuda:{device}")
     if distributed:
         dist.all_reduce(totals, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        ext_r0 = ext.clone()
     closest_all, shadow_all, samples_all = [float(x) for x in totals.tolist()]
     elapsed = float(tmax.item())
 
     if rank == 0:
         rays = closest_all + shadow_all
         mrays = rays / elapsed / 1e6
-        # roofline of k_extend on rank 0's stream
-        ext_ms, ext_launches, ext_rays = [float(x) for x in ext.tolist()]
-        mean_launch_s = (ext_ms / 1e3) / max(ext_launches, 1.0)
-        rays_per_launch = ext_rays / max(ext_launches, 1.0)
-        achieved = EXTEND_BYTES_PER_RAY * rays_per_launch / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
-        traffic = None
+        # Roofline of the dominant kernel (most event-timed GPU time in the timed region) on rank 0.
+        # Each stage's begin/end HIP events are recorded on the stream of the partition that
+        # launched it, so with 4 partitions in flight a launch's duration includes the GPU
+        # time it shares with the other partitions' kernels: `concurrency` says how many
+        # kernels ran at once on average, and `isolated` gives the serialized figures
+        # (rocprofv3 --pmc runs, profiles/traffic.json) for the same kernel.
+        units = {"generate": samples, "extend": traced, "shade": closest, "connect": traced_sh, "splat": samples}
+        dom = max(BYTES_PER_UNIT, key=lambda k: kms[STAGES.index(k)])
+        di = STAGES.index(dom)
+        mean_launch_s = (kms[di] / 1e3) / max(kl[di], 1)
+        units_per_launch = units[dom] / max(kl[di], 1)
+        alg_bytes = BYTES_PER_UNIT[dom] * units_per_launch
+        achieved = alg_bytes / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
+        traffic = isolated = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("config") == args.config and tj.get("kernel") == "k_extend":
-                traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
+            ent = tj.get("kernels", {}).get(KERNEL[dom]) if tj.get("config") == args.config else None
+            if ent:
+                traffic = ent["hbm_bytes_per_launch"]
+                iso_gbs = alg_bytes / (ent["isolated_mean_us"] * 1e-6) / 1e9
+                isolated = {"mean_launch_ms": round(ent["isolated_mean_us"] / 1e3, 4), "achieved": round(iso_gbs, 1),
+                            "frac": round(iso_gbs / HBM_PEAK_GBS, 4), "source": tj.get("source")}
+        except (OSError, ValueError, KeyError):
             pass
+        concurrency = sum(kms[:5]) / (elapsed * 1e3) if elapsed > 0 else 0.0
+        pipe_bytes = PIPE_BYTES_PER_RAY * (closest + shadow) + PIPE_BYTES_PER_SAMPLE * samples
+        pipe_gbs = pipe_bytes / elapsed / 1e9
         # output pass on the resolved frame: k_post, 16 B read + 4 B written per pixel
         bgra = torch.empty((h, w), dtype=torch.int32, device=f"cuda:{device}")
         pcall = lambda: rt.lib().rt_postprocess_device(device, C.c_void_p(accum.data_ptr()), w, h, C.byref(post), 0,
@@ -257,9 +285,13 @@ def main():
                        "parallelism": f"tiles%{world}" + ("+rccl_reduce" if world > 1 else "")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "kernel": "k_extend", "bytes_per_ray": EXTEND_BYTES_PER_RAY,
+                         "kernel": KERNEL[dom], "bytes_per_unit": BYTES_PER_UNIT[dom],
+                         "units_per_launch": round(units_per_launch, 1),
                          "mean_launch_ms": round(mean_launch_s * 1e3, 4),
-                         "traced_rays_per_launch": round(rays_per_launch, 1)},
+                         "concurrency": round(concurrency, 2), "isolated": isolated,
+                         "pipeline": {"bytes": pipe_bytes, "achieved": round(pipe_gbs, 1),
+                                      "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
+                                      "formula": "152 B x (closest + shadow rays) + 144 B x samples, rank 0, / wall time"}},
             "stage_ms_per_step": {n: round(kms[i] / args.steps, 2) for i, n in
                                   enumerate(["generate", "extend", "shade", "connect", "splat", "resolve"])},
             "cpu_baseline": cpu,

@@ -1525,9 +1525,9 @@ __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Coun
 // adjacent columns, so at every step they read 64 adjacent records of one
 // sample plane (record = s*P + p): the loads stay coalesced.
 #ifndef RT_RES_RY
-#define RT_RES_RY 8
+#define RT_RES_RY 4
 #endif
-constexpr int RES_RY = RT_RES_RY;
+constexpr int RES_RY = RT_RES_RY;      // 4: measured best of 2, 4, 6, 8, 16 (C3 256 spp: 30 ms)
 constexpr int RES_BX = 64, RES_BY = 4;
 __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
     __shared__ float lut[512];

@@ -17,6 +17,7 @@ import os
 
 KERNELS = ["k_generate", "k_trace<false>", "k_shade", "k_trace<true>", "k_splat", "k_resolve", "k_bookkeep"]
 LABEL = {"k_trace<false>": "k_extend (k_trace<false>)", "k_trace<true>": "k_connect (k_trace<true>)"}
+KEYS = {"k_trace<false>": "k_extend", "k_trace<true>": "k_connect"}
 
 
 def short(name):
@@ -86,19 +87,19 @@ def main():
     if a.out:
         open(a.out, "w").write(text)
         json.dump(out, open(os.path.splitext(a.out)[0] + ".json", "w"), indent=1)
-    if a.traffic and "k_trace<false>" in out:
-        e = out["k_trace<false>"]
-        rec = {"config": "c3", "kernel": "k_extend",
-               "hbm_bytes_per_launch": (e["hbm_read_mb_per_launch"] + e["hbm_write_mb_per_launch"]) * 1e6,
-               "source": a.tag_dir, "note": "2 x FETCH_SIZE + WRITE_SIZE per k_trace<false> launch (rocprofv3 --pmc)"}
+    if a.traffic and out:
+        rec = {"config": "c3", "source": a.tag_dir,
+               "note": "HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc, kernels serialized), "
+                       "plus the serialized mean launch duration",
+               "kernels": {KEYS.get(k, k): {"hbm_bytes_per_launch": (e["hbm_read_mb_per_launch"] + e["hbm_write_mb_per_launch"]) * 1e6,
+                                            "isolated_mean_us": e["mean_us"], "dispatches": e["dispatches"]}
+                           for k, e in out.items()}}
         if a.bench_log and os.path.exists(a.bench_log):
             for line in open(a.bench_log):
                 if line.startswith("{"):
-                    b = json.loads(line)
-                    rec["bench_spp"] = b["config"].get("spp")
-                    rec["traced_rays_per_launch"] = b["roofline"].get("traced_rays_per_launch", b["roofline"].get("rays_per_launch"))
+                    rec["bench_spp"] = json.loads(line)["config"].get("spp")
         json.dump(rec, open(a.traffic, "w"), indent=1)
-        print("wrote", a.traffic, rec)
+        print("wrote", a.traffic)
 
 
 if __name__ == "__main__":
