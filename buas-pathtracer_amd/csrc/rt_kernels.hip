@@ -342,6 +342,14 @@ constexpr int FETCH_Q = (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u);   // float4 per l
 // ray is queued with MLIST_FULL and the kernel re-walks the whole top level
 // (re-testing an analytic primitive at equal t changes nothing: strict tests).
 constexpr uint32_t MLIST_MAX = 4;
+// a load whose address is the same in every active lane, its value moved to SGPRs
+RT_D float4 ld_uniform(const float4* p) {
+    const float4 v = *p;
+    return make_float4(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
+                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y))),
+                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z))),
+                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w))));
+}
 constexpr uint32_t MLIST_FULL = 0xFFFFFFFFu;
 struct Prologue { float t; uint32_t code; bool occluded, bvh; V3 inv_d; uint32_t mlist; };
 RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ, uint32_t ignored) {
@@ -364,6 +372,62 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
         r.bvh = bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn) && tn < r.t;
         return r;
     }
+#ifndef RT_PROLOGUE_UNIFORM
+#define RT_PROLOGUE_UNIFORM 1
+#endif
+#if RT_PROLOGUE_UNIFORM
+    // Wave-uniform walk: every lane follows octant 0's sequence, so entry and record
+    // addresses are the same across the wave (one cache line per load, values moved to
+    // SGPRs) and the lanes stay converged; each lane tests only the entries on its own
+    // path (`next`).  Octant 0's order differs from the reference's front-to-back order
+    // only in which of two surfaces at exactly equal t is kept (see above).
+    const float4* seq = sc.top_seq;
+    uint32_t list = 0, n = 0, next = 0;
+    bool full = false;
+    const uint32_t len = sc.top_seq_len;
+    for (uint32_t i = 0; i < len; ++i) {
+        const float4 a = ld_uniform(seq + 2*i), b = ld_uniform(seq + 2*i + 1);
+        const uint32_t info = __float_as_uint(b.z), skip = __float_as_uint(b.w);
+        bool pass = false;
+        if (next == i) {
+            float tn;
+            pass = bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn) && tn < r.t;
+            next = pass ? ((info >> 31) ? skip : i + 1) : skip;
+        }
+        if (!(info >> 31) || __ballot(pass) == 0ull) continue;
+        const uint32_t first = info & 0xFFFFFFu, end = first + ((info >> 24) & 127u);
+        for (uint32_t j = first; j < end; ++j) {                   // the leaf's primitives in order
+            const float4* q = sc.leaf_rec + (size_t)j*LEAF_REC_Q;
+            const float4 q3 = ld_uniform(q + 3);
+            const uint32_t pi = __float_as_uint(q3.x), type = __float_as_uint(q3.y);
+            if (!pass || pi == ignored) continue;
+            M34 inv;
+            const float4 q0 = ld_uniform(q), q1 = ld_uniform(q + 1), q2 = ld_uniform(q + 2);
+            inv.e[0][0] = q0.x; inv.e[0][1] = q0.y; inv.e[0][2] = q0.z; inv.e[0][3] = q0.w;
+            inv.e[1][0] = q1.x; inv.e[1][1] = q1.y; inv.e[1][2] = q1.z; inv.e[1][3] = q1.w;
+            inv.e[2][0] = q2.x; inv.e[2][1] = q2.y; inv.e[2][2] = q2.z; inv.e[2][3] = q2.w;
+            const Ray ir = make_ray(xform(inv, o, 1.0f), xform(inv, d, 0.0f), 0.0f);   // transform_ray :403-409
+            if (type == RT_PRIMITIVE_MESH) {                       // the mesh root's pop-time test (:269-275)
+                const float4 q4 = ld_uniform(q + 4), q5 = ld_uniform(q + 5);
+                float tm;
+                if (bv_static(ir, {q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z}, tm) && tm < r.t) {
+                    if (n < sc.mlist_max) list |= j << (6*n);
+                    else full = true;
+                    ++n;
+                }
+                continue;
+            }
+            bool hit = false;
+            if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, q3.z, r.t);
+            else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {q3.z, q3.w, ld_uniform(q + 4).x}, r.t);
+            if (hit) {
+                r.code = pi;
+                if (occ) { r.occluded = true; pass = false; next = 0xFFFFFFFFu; }
+            }
+        }
+    }
+    if (r.occluded) return r;
+#else
     const float4* seq = sc.top_seq + 2*(size_t)sc.top_seq_len*(wr.neg & 7u);
     uint32_t list = 0, n = 0;
     bool full = false;
@@ -405,6 +469,7 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
         }
         i = skip;
     }
+#endif
     r.bvh = n > 0;
     r.mlist = full ? MLIST_FULL : (list | (n << 24));
     return r;
@@ -1375,12 +1440,7 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
                                 sh_d = Lv;
                                 sh_t = dist - 2*EPSILON;
                                 sh_light = lid;
-                                cast_shadow = true;
-                                // intersect_shadow_ray (:756): planes and the root here; only rays
-                                // that enter the BVH are queued for k_trace<true>
-                                spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, lid);
-                                shadow = !spro.occluded && spro.bvh;
-                                if (!spro.occluded && !spro.bvh) total = add(total, sh_c);   // :768
+                                cast_shadow = true;                 // traced below, lanes reconverged
                             }
                         }
                     }
@@ -1412,9 +1472,17 @@ __global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, Fr
             total = add(total, mul(thr, sample_sky(sc, rd)));                 // miss :812-815
             done = true;
         }
+        if (cast_shadow) {
+            // intersect_shadow_ray (:756): planes and the top level here; only rays that meet
+            // a mesh are queued for k_trace<true>.  Nothing else adds to total_color after the
+            // NEE term in a bounce, so adding it here keeps the reference's order (:768).
+            spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
+            shadow = !spro.occluded && spro.bvh;
+            if (!spro.occluded && !spro.bvh) total = add(total, sh_c);
+        }
         cont = !done;
         nro = ro; nrd = rd;
-        if (cont) {                                        // next bounce's intersect_scene: planes + root here
+        if (cont) {                                        // next bounce's intersect_scene: planes + top level here
             cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
             pool.hit[slot] = make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f);
             pool.hit_w[slot] = 0.0f;

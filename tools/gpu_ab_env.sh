@@ -15,7 +15,7 @@ for v in "$@"; do
   env $v timeout -k 10 300 python bench.py $ARGS > gpurun_out/ab_$i.log 2>&1
   rc=$?; echo "== [$v] rc=$rc"; tail -1 gpurun_out/ab_$i.log | python -c 'import json,sys
 try:
-  d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["stage_ms_per_step"], d["roofline"]["traced_rays_per_launch"])
+  d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["stage_ms_per_step"], d["roofline"]["kernel"], d["roofline"]["concurrency"])
 except Exception as e: print("parse error", e)'
   [ $rc -ne 0 ] && exit $rc
 done
