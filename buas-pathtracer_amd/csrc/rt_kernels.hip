@@ -77,6 +77,7 @@ struct DevScene {
     const float* normals;           // 9 floats per triangle, ORIGINAL order (same offsets)
     const rt_bvh_node* mnodes;      // all mesh BVH nodes (child indices mesh-local), traversal layout
     const rt_bvh_node* mnodes_src;  // the same in the caller's layout
+    const float4* mnodes4;          // mesh BVH4 nodes (MESH_BVH4), 8 float4 each, global indices
     const float* sky;               // 3 floats per pixel
     uint32_t sky_w, sky_h;
     V3 top_sky, bot_sky;
@@ -320,7 +321,21 @@ enum { TM_TOP = 0, TM_LEAF = 1, TM_MESH = 2, TM_DONE = 3 };
 // top-level leaf record), then the arithmetic.  Lanes doing different kinds of
 // work in the same step therefore share one memory latency.
 constexpr uint32_t TRI_FETCH = RT_TRI_BATCH;
-constexpr int FETCH_Q = (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u);   // float4 per lane per step
+// Mesh BVHs are traversed as BVH4: each interior node of the caller's BVH2 is
+// merged with its interior children (built at upload, build_bvh4).  A node holds
+// up to 4 children in SoA form, one 128-byte line:
+//   F[0..2] = bv_p.x/y/z of children 0-3, F[3..5] = bv_r.x/y/z, F[6] = their packed
+//   records (EMPTY4: no child), F[7].x = split axes: bits 0-1 the BVH2 node's,
+//   2-3 its left child's (children 0,1), 4-5 its right child's (children 2,3).
+// The children are visited in exactly the BVH2 depth-first order (the reference's
+// front-to-back order by d_is_negative, RT/intersection.cpp:328-340); the BVH2
+// level in between is skipped, i.e. its box test, which only culls what its
+// children's own tests cull (their boxes lie inside it).  Halves the interior steps.
+#ifndef RT_MESH_BVH4
+#define RT_MESH_BVH4 1
+#endif
+constexpr uint32_t EMPTY4 = 0xFFFFFFFFu;
+constexpr int FETCH_Q = (RT_MESH_BVH4 ? 8 : (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u));   // float4 per lane per step
 
 // The part of intersect_scene_internal (RT/intersection.cpp:411-598) that needs
 // no BVH: the planes, brute force (:424-433), then the top-level root, which the
@@ -591,11 +606,40 @@ struct Traversal {
         return false;
     }
 
+    // children of a mesh BVH4 node F[0..7], pushed so they pop in the BVH2 depth-first order
+    template <bool SH, bool FIN>
+    RT_D void push_children4(const Stack& st, const float4* F) {
+        const Ray r = cur_ray();
+        const uint32_t meta = __float_as_uint(F[7].x), nb = cflags & 7u;
+        const uint32_t g = (nb >> (meta & 3u)) & 1u;               // group visited first: 1 = the right pair
+        const uint32_t fa = (nb >> ((meta >> 2) & 3u)) & 1u;       // left pair: child 1 first
+        const uint32_t fb = (nb >> ((meta >> 4) & 3u)) & 1u;       // right pair: child 3 first
+        const uint32_t rec[4] = {__float_as_uint(F[6].x), __float_as_uint(F[6].y), __float_as_uint(F[6].z), __float_as_uint(F[6].w)};
+        float tn[4];
+        bool h[4];
+        h[0] = bv_static<FIN>(r, {F[0].x, F[1].x, F[2].x}, {F[3].x, F[4].x, F[5].x}, tn[0]) && rec[0] != EMPTY4;
+        h[1] = bv_static<FIN>(r, {F[0].y, F[1].y, F[2].y}, {F[3].y, F[4].y, F[5].y}, tn[1]) && rec[1] != EMPTY4;
+        h[2] = bv_static<FIN>(r, {F[0].z, F[1].z, F[2].z}, {F[3].z, F[4].z, F[5].z}, tn[2]) && rec[2] != EMPTY4;
+        h[3] = bv_static<FIN>(r, {F[0].w, F[1].w, F[2].w}, {F[3].w, F[4].w, F[5].w}, tn[3]) && rec[3] != EMPTY4;
+        // visit order: first pair (2g + its first, 2g + its second), then the other pair; push reversed
+        const uint32_t f1 = g ? fb : fa, f2 = g ? fa : fb;
+        const uint32_t v[4] = {2u*g + f1, 2u*g + 1u - f1, 2u*(1u - g) + f2, 2u*(1u - g) + 1u - f2};
+#pragma unroll
+        for (int k = 3; k >= 0; --k) {
+            const uint32_t i = v[k];
+            const bool hi = i == 0 ? h[0] : i == 1 ? h[1] : i == 2 ? h[2] : h[3];
+            const uint32_t ri = i == 0 ? rec[0] : i == 1 ? rec[1] : i == 2 ? rec[2] : rec[3];
+            const float ti = i == 0 ? tn[0] : i == 1 ? tn[1] : i == 2 ? tn[2] : tn[3];
+            if (hi) push<SH>(st, ri, ti);
+        }
+    }
+
     // One traversal step; returns false once the query is finished (mode == TM_DONE).
-    // A step pops before it pushes and pushes at most two entries, so when no lane of
-    // the wave is within two levels of STACK_LDS the whole step stays in LDS.
+    // A step pops before it pushes and pushes at most PUSH_MAX entries, so when no lane of
+    // the wave is within PUSH_MAX levels of STACK_LDS the whole step stays in LDS.
+    static constexpr int PUSH_MAX = RT_MESH_BVH4 ? 4 : 2;
     RT_D bool step(const DevScene& sc, const Stack& st) {
-        if (__ballot(sp > STACK_LDS - 2 || !(cflags & 64u)) == 0ull) return step_impl<true, true>(sc, st);
+        if (__ballot(sp > STACK_LDS - PUSH_MAX || !(cflags & 64u)) == 0ull) return step_impl<true, true>(sc, st);
         return step_impl<false, false>(sc, st);
     }
     template <bool SH, bool FIN>
@@ -625,7 +669,11 @@ struct Traversal {
             src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
         } else {                                                   // interior: the sibling pair
             RT_STAT(4);
-            src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4;
+#if RT_MESH_BVH4
+            if (mode == TM_MESH) { src = sc.mnodes4 + 8*(size_t)cur_lf; nq = 8; }
+            else
+#endif
+            { src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4; }
         }
         // unconditional: every array the step reads is padded by FETCH_Q float4 at upload
         (void)nq;
@@ -679,6 +727,10 @@ struct Traversal {
             else has_cur = false;
             return true;
         }
+#if RT_MESH_BVH4
+        if (mode == TM_MESH) push_children4<SH, FIN>(st, F);
+        else
+#endif
         push_children<SH, FIN>(st, F);
         has_cur = false;
         return true;
@@ -1201,11 +1253,12 @@ constexpr uint32_t CHUNK = 256;
 #endif
 constexpr int STEPS_PER_REFILL = RT_STEPS_PER_REFILL;
 
-#ifdef RT_TRACE_WAVES
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
-#else
-#define RT_TRACE_ATTR
+// 4 waves per SIMD (128 VGPRs): the BVH4 step wants ~138, i.e. 3 waves; the few
+// spilled values cost less than the lost occupancy (C3: 5446 vs 5389 Mrays/s)
+#ifndef RT_TRACE_WAVES
+#define RT_TRACE_WAVES 4
 #endif
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
 template <bool OCC>
 __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag) {
     __shared__ uint2 lds_stack[STACK_LDS*TB];
@@ -1308,7 +1361,12 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 }
 
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
-__global__ void __launch_bounds__(BLOCK) k_shade(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
+#ifdef RT_SHADE_WAVES
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WAVES)))
+#else
+#define RT_SHADE_ATTR
+#endif
+__global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur) {
     __shared__ uint32_t agg[BLOCK / 64 + 1];
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
@@ -1931,6 +1989,58 @@ std::vector<float4> top_sequences(const rt_bvh_node* nodes, uint32_t count, uint
     return out;
 }
 
+// Mesh BVH4 (see RT_MESH_BVH4): node k for the BVH2 interior node i holds i's
+// children, each replaced by its own two children when it is interior.  Interior
+// records are global BVH4 indices (`base` + local); leaves keep the BVH2 packed
+// record (or its index form, mesh-local).  `need` = an upper bound of the stack
+// entries a traversal below this node can hold.  Returns the node's record.
+uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, uint32_t base, std::vector<float4>& out,
+                    uint32_t& need, bool& ok) {
+    const uint32_t k = (uint32_t)(out.size() / 8);
+    out.resize(out.size() + 8, make_float4(0, 0, 0, 0));
+    uint32_t slot[4] = {EMPTY4, EMPTY4, EMPTY4, EMPTY4};
+    uint32_t meta = n[i].split_axis & 3u;
+    auto interior = [&](uint32_t c) { return n[c].count == 0 && n[c].left_first != 0 && n[c].left_first + 1 < count; };
+    if (interior(i) || (i == 0 && n[0].count == 0 && n[0].left_first + 1 < count && n[0].left_first != 0)) {
+        for (uint32_t g = 0; g < 2; ++g) {
+            const uint32_t c = n[i].left_first + g;
+            if (interior(c)) {
+                slot[2*g] = n[c].left_first; slot[2*g + 1] = n[c].left_first + 1;
+                meta |= (n[c].split_axis & 3u) << (2 + 2*g);
+            } else {
+                slot[2*g] = c;
+            }
+        }
+    }
+    float4 q[8];
+    for (int j = 0; j < 8; ++j) q[j] = make_float4(0, 0, 0, 0);
+    uint32_t nchild = 0, deeper = 0;
+    for (int j = 0; j < 4; ++j) {
+        uint32_t rec = EMPTY4;
+        if (slot[j] != EMPTY4) {
+            const uint32_t m = slot[j];
+            const rt_bvh_node& c = n[m];
+            (&q[0].x)[j] = c.bv_p.x; (&q[1].x)[j] = c.bv_p.y; (&q[2].x)[j] = c.bv_p.z;
+            (&q[3].x)[j] = c.bv_r.x; (&q[4].x)[j] = c.bv_r.y; (&q[5].x)[j] = c.bv_r.z;
+            ++nchild;
+            if (interior(m)) {
+                uint32_t cn = 0;
+                rec = build_bvh4(n, count, m, base, out, cn, ok);
+                deeper = std::max(deeper, cn);
+            } else {
+                rec = pack_node(m, c.left_first, c.count, 0);
+                if (!(rec & 0x80000000u) && !((rec >> 30) & 1u)) rec = 0x80000000u | m;   // never an interior form
+            }
+        }
+        memcpy(&(&q[6].x)[j], &rec, 4);
+    }
+    memcpy(&q[7].x, &meta, 4);
+    for (int j = 0; j < 8; ++j) out[8*(size_t)k + j] = q[j];
+    need = (nchild ? nchild - 1 : 0) + deeper;
+    if (base + k >= (1u << 28)) ok = false;
+    return base + k;
+}
+
 uint32_t tree_depth(const rt_bvh_node* nodes, uint32_t count) {
     if (!count) return 0;
     uint32_t maxd = 0;
@@ -2299,6 +2409,8 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     std::vector<float> normals;
     std::vector<rt_bvh_node> mnodes;
     uint32_t mesh_depth = 0;
+    std::vector<float4> mnodes4;
+    std::vector<uint32_t> root4(d->mesh_count, 0u);
     for (uint32_t m = 0; m < d->mesh_count; ++m) {
         const rt_mesh& M = d->meshes[m];
         meshes[m].tri_offset = (uint32_t)orig.size();
@@ -2310,7 +2422,23 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 set_error("mesh BVH node out of range"); return fail(RT_ERROR_INVALID);
             }
         }
+#if RT_MESH_BVH4
+        if (M.node_count) {
+            const rt_bvh_node& r0 = M.nodes[0];
+            if (r0.count) {
+                root4[m] = pack_node(0u, r0.left_first, r0.count, 0u);
+                mesh_depth = std::max(mesh_depth, 1u);
+            } else {
+                bool ok = true;
+                uint32_t need = 0;
+                root4[m] = build_bvh4(M.nodes, M.node_count, 0u, (uint32_t)(mnodes4.size() / 8), mnodes4, need, ok);
+                if (!ok) { set_error("mesh BVH too large for the BVH4 records"); return fail(RT_ERROR_INVALID); }
+                mesh_depth = std::max(mesh_depth, need + 1);
+            }
+        }
+#else
         mesh_depth = std::max(mesh_depth, tree_depth(M.nodes, M.node_count));
+#endif
         for (uint32_t t = 0; t < M.triangle_count; ++t) {
             const rt_v3* v = M.triangles + 3*(size_t)t;
             tris.push_back(make_float4(v[0].x, v[0].y, v[0].z, 0.0f));
@@ -2355,7 +2483,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 const rt_mesh& M = d->meshes[p.mesh_index];
                 rt_bvh_node rn = {};
                 if (M.node_count) rn = M.nodes[0];
+#if RT_MESH_BVH4
+                const uint32_t root = root4[p.mesh_index];
+#else
                 const uint32_t root = pack_node(0u, rn.left_first, rn.count, rn.split_axis);
+#endif
                 q[3] = make_float4(u2f(pi), u2f(p.type), u2f(meshes[p.mesh_index].node_offset), u2f(meshes[p.mesh_index].tri_offset));
                 q[4] = make_float4(u2f(root), rn.bv_p.x, rn.bv_p.y, rn.bv_p.z);
                 q[5] = make_float4(rn.bv_r.x, rn.bv_r.y, rn.bv_r.z, 0.0f);
@@ -2383,6 +2515,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             std::copy(one.begin(), one.end(), tl.begin() + off);
         }
         if ((err = upload(s, tl.data(), tl.size(), &ds.mnodes))) return fail(err);
+    }
+    ds.mnodes4 = nullptr;
+    if (!mnodes4.empty()) {
+        mnodes4.resize(mnodes4.size() + FETCH_Q, make_float4(0, 0, 0, 0));
+        if ((err = upload(s, mnodes4.data(), mnodes4.size(), &ds.mnodes4))) return fail(err);
     }
     if (d->skydome && d->skydome_w && d->skydome_h) {
         if ((err = upload(s, reinterpret_cast<const float*>(d->skydome), 3*(size_t)d->skydome_w*d->skydome_h, &ds.sky))) return fail(err);
