@@ -83,7 +83,38 @@ struct DevScene {
     V3 top_sky, bot_sky;
     const uint8_t* strata;          // g_strata_permutation_sets [256][64]
     const uint8_t* bluenoise;       // sobol | scrambling | ranking
+    // The small tables above (materials, primitives, planes, transforms, lights,
+    // top-level sequence and records, meshes, strata) packed into one blob that the
+    // slot-ordered kernels copy into LDS at start (scene_in_lds); 0 = too large.
+    const float4* blob;
+    uint32_t blob_q;                // float4 count (<= LDS_SCENE_Q)
+    uint32_t off[10];               // byte offsets of the tables in the blob (BLOB_*)
 };
+enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_TOP_SEQ, BLOB_LEAF_REC,
+       BLOB_MESHES, BLOB_STRATA, BLOB_COUNT };
+constexpr uint32_t LDS_SCENE_Q = 2048;   // 32 KB
+
+// The scene seen through the LDS copy: every small table's pointer rebased onto
+// `lds` (generic pointers, so the code that reads them is unchanged).  All
+// threads of the block must call it.
+RT_D DevScene scene_in_lds(const DevScene& sc, float4* lds) {
+    if (!sc.blob_q) return sc;
+    for (uint32_t i = threadIdx.x; i < sc.blob_q; i += blockDim.x) lds[i] = sc.blob[i];
+    __syncthreads();
+    DevScene s = sc;
+    const char* b = reinterpret_cast<const char*>(lds);
+    s.materials = reinterpret_cast<const rt_material*>(b + sc.off[BLOB_MATERIALS]);
+    s.prims = reinterpret_cast<const rt_primitive*>(b + sc.off[BLOB_PRIMS]);
+    s.planes = reinterpret_cast<const rt_primitive*>(b + sc.off[BLOB_PLANES]);
+    s.inv = reinterpret_cast<const M34*>(b + sc.off[BLOB_INV]);
+    s.fwd = reinterpret_cast<const M34*>(b + sc.off[BLOB_FWD]);
+    s.lights = reinterpret_cast<const uint32_t*>(b + sc.off[BLOB_LIGHTS]);
+    if (sc.top_seq) s.top_seq = reinterpret_cast<const float4*>(b + sc.off[BLOB_TOP_SEQ]);
+    s.leaf_rec = reinterpret_cast<const float4*>(b + sc.off[BLOB_LEAF_REC]);
+    s.meshes = reinterpret_cast<const DevMesh*>(b + sc.off[BLOB_MESHES]);
+    s.strata = reinterpret_cast<const uint8_t*>(b + sc.off[BLOB_STRATA]);
+    return s;
+}
 
 struct Ray { V3 o, d, inv_d; uint32_t neg; float max_t; uint32_t zero; };   // zero: axes with d == 0
 
@@ -1153,9 +1184,11 @@ constexpr int BLOCK = 512;          // slot-ordered kernels (generate / shade / 
 constexpr int EV_SLOTS = 4;     // iterations between host syncs in run_frame
 
 // k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
-__global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
+__global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                     Counters* cnt, int cur) {
     __shared__ uint32_t agg[BLOCK / 64 + 1];
+    __shared__ float4 lds_scene[LDS_SCENE_Q];
+    const DevScene sc = scene_in_lds(sc_g, lds_scene);
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const bool want = slot < pool.n && pool.state[slot] == S_FREE;
     // free slots claim consecutive sample numbers in slot order: the block's first
@@ -1366,9 +1399,11 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 #else
 #define RT_SHADE_ATTR
 #endif
-__global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc, rt_settings st, FrameParams fp, Pool pool,
+__global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur) {
     __shared__ uint32_t agg[BLOCK / 64 + 1];
+    __shared__ float4 lds_scene[LDS_SCENE_Q];
+    const DevScene sc = scene_in_lds(sc_g, lds_scene);
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const bool valid = slot < pool.n && pool.state[slot] == S_TRACE;   // traced this iteration
     bool cont = false, done = false, shadow = false, cast_shadow = false, enq = false;
@@ -2389,9 +2424,10 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         if ((err = upload(s, tl.data(), tl.size(), &ds.bvh))) return fail(err);
     }
     if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
+    std::vector<float4> top_seq_host, leaf_rec_host;
     {
         const char* env = getenv("RT_TOP_PROLOGUE");              // 0: the trace kernels walk the top level
-        std::vector<float4> seq;
+        std::vector<float4>& seq = top_seq_host;
         uint32_t len = 0;
         if (!(env && env[0] == '0')) seq = top_sequences(d->bvh_nodes, d->bvh_node_count, d->bvh_index_count, len);
         ds.top_seq = nullptr; ds.top_seq_len = 0; ds.mlist_max = MLIST_MAX;
@@ -2498,6 +2534,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         }
         rec.resize(rec.size() + FETCH_Q, make_float4(0, 0, 0, 0));
         if ((err = upload(s, rec.data(), rec.size(), &ds.leaf_rec))) return fail(err);
+        leaf_rec_host = rec;
     }
     if ((err = upload(s, meshes.data(), meshes.size(), &ds.meshes))) return fail(err);
     tris.resize(tris.size() + FETCH_Q, make_float4(0, 0, 0, 0));
@@ -2529,6 +2566,32 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     ds.bot_sky = rv3(d->bot_sky_color);
     if ((err = upload(s, rt_dev_strata_tab, sizeof(rt_dev_strata_tab), &ds.strata))) return fail(err);
     if ((err = upload(s, rt_dev_bluenoise_tab, sizeof(rt_dev_bluenoise_tab), &ds.bluenoise))) return fail(err);
+    {   // the LDS blob (scene_in_lds): the small tables, 16-byte aligned, when they fit
+        std::vector<uint8_t> blob;
+        auto put = [&](int which, const void* p, size_t bytes) {
+            ds.off[which] = (uint32_t)blob.size();
+            if (bytes) blob.insert(blob.end(), (const uint8_t*)p, (const uint8_t*)p + bytes);
+            blob.resize((blob.size() + 15) & ~(size_t)15, 0);
+        };
+        put(BLOB_MATERIALS, mats.data(), mats.size()*sizeof(rt_material));
+        put(BLOB_PRIMS, d->primitives, (size_t)d->primitive_count*sizeof(rt_primitive));
+        put(BLOB_PLANES, d->planes, (size_t)d->plane_count*sizeof(rt_primitive));
+        put(BLOB_INV, inv.data(), inv.size()*sizeof(M34));
+        put(BLOB_FWD, fwd.data(), fwd.size()*sizeof(M34));
+        put(BLOB_LIGHTS, d->lights, (size_t)d->light_count*sizeof(uint32_t));
+        put(BLOB_TOP_SEQ, top_seq_host.data(), top_seq_host.size()*sizeof(float4));
+        put(BLOB_LEAF_REC, leaf_rec_host.data(), (size_t)d->bvh_index_count*LEAF_REC_Q*sizeof(float4));
+        put(BLOB_MESHES, meshes.data(), meshes.size()*sizeof(DevMesh));
+        put(BLOB_STRATA, rt_dev_strata_tab, sizeof(rt_dev_strata_tab));
+        const char* env = getenv("RT_LDS_SCENE");               // 0: the kernels read the tables from HBM
+        ds.blob = nullptr; ds.blob_q = 0;
+        if (blob.size() <= 16*(size_t)LDS_SCENE_Q && !(env && env[0] == '0')) {
+            std::vector<float4> q(blob.size() / 16);
+            memcpy(q.data(), blob.data(), blob.size());
+            if ((err = upload(s, q.data(), q.size(), &ds.blob))) return fail(err);
+            ds.blob_q = (uint32_t)q.size();
+        }
+    }
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("hipGetDeviceProperties"); return fail(RT_ERROR_DEVICE); }
