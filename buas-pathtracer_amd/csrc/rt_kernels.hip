@@ -74,7 +74,7 @@ struct DevScene {
     const DevMesh* meshes;
     const float4* tris;             // 3 float4 per triangle: a, b-a, c-a (BVH order, all meshes)
     const uint32_t* tri_orig;       // mesh-local original triangle index per BVH slot
-    const float* normals;           // 9 floats per triangle, ORIGINAL order (same offsets)
+    const float* normals;           // 9 floats per triangle, BVH slot order (same index as tris)
     const rt_bvh_node* mnodes;      // all mesh BVH nodes (child indices mesh-local), traversal layout
     const rt_bvh_node* mnodes_src;  // the same in the caller's layout
     const float4* mnodes4;          // mesh BVH4 nodes (MESH_BVH4), 8 float4 each, global indices
@@ -791,8 +791,7 @@ RT_D void hit_geometry(const DevScene& sc, const Ray& ray, const Hit& h, V3& I, 
             const DevMesh mesh = sc.meshes[prim.mesh_index];
             float u = 1.0f - h.v - h.w;
             if (mesh.has_normals) {
-                uint32_t orig = sc.tri_orig[h.tri];
-                const float* nt = sc.normals + 9*(size_t)(mesh.tri_offset + orig);
+                const float* nt = sc.normals + 9*(size_t)h.tri;                 // BVH slot order
                 n = add(add(smul(u, {nt[0], nt[1], nt[2]}), smul(h.v, {nt[3], nt[4], nt[5]})),
                         smul(h.w, {nt[6], nt[7], nt[8]}));
             } else {
@@ -1047,6 +1046,7 @@ struct FrameParams {
     uint32_t ntiles;
     const uint32_t* tile_ids;       // owned tiles
     const uint32_t* tile_prefix;    // [ntiles+1] pixel prefix sums
+    const uint32_t* pix_xy;         // [P]: x | y << 16 of tile-list pixel p (k_pixel_map)
     // explicit sample list mode (rt_trace_samples)
     const uint32_t* list_xy;
     const uint32_t* list_s;
@@ -1183,6 +1183,18 @@ RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return b
 constexpr int BLOCK = 512;          // slot-ordered kernels (generate / shade / splat)
 constexpr int EV_SLOTS = 4;     // iterations between host syncs in run_frame
 
+// k_pixel_map — the coordinates of every pixel of the shard's tile list, in list
+// order (tiles descending, raster inside a tile: RT/raytracer.cpp:555, :409-410),
+// so k_generate maps a sample to its pixel with one coalesced load.  One block per tile.
+__global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out) {
+    const uint32_t i = blockIdx.x;
+    const uint32_t tile = fp.tile_ids[i], base = fp.tile_prefix[i], n = fp.tile_prefix[i + 1] - base;
+    const uint32_t min_x = fp.tile_w*(tile % fp.tcx), min_y = fp.tile_h*(tile / fp.tcx);
+    const uint32_t tw = min(fp.w, min_x + fp.tile_w) - min_x;
+    for (uint32_t local = threadIdx.x; local < n; local += 256)
+        out[base + local] = (min_x + local % tw) | ((min_y + local / tw) << 16);
+}
+
 // k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
 __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                     Counters* cnt, int cur) {
@@ -1205,15 +1217,16 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         if (fp.list_xy) {
             x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
         } else {
-            uint32_t pass = (uint32_t)(k / fp.pixels);
-            p = (uint32_t)(k % fp.pixels);
-            uint32_t lo = 0, hi = fp.ntiles;                 // tile_prefix[lo] <= p < tile_prefix[lo+1]
-            while (hi - lo > 1) { uint32_t mid = (lo + hi) >> 1; if (fp.tile_prefix[mid] <= p) lo = mid; else hi = mid; }
-            uint32_t tile = fp.tile_ids[lo];
-            uint32_t local = p - fp.tile_prefix[lo];
-            uint32_t min_x = fp.tile_w*(tile % fp.tcx), min_y = fp.tile_h*(tile / fp.tcx);
-            uint32_t tw = min(fp.w, min_x + fp.tile_w) - min_x;
-            x = min_x + local % tw; y = min_y + local / tw; s = pass;
+            uint32_t pass;
+            if (k < 0x100000000ull) {                        // 32-bit division when it suffices
+                pass = (uint32_t)k / fp.pixels;
+                p = (uint32_t)k - pass*fp.pixels;
+            } else {
+                pass = (uint32_t)(k / fp.pixels);
+                p = (uint32_t)(k % fp.pixels);
+            }
+            const uint32_t xy = fp.pix_xy[p];                // the tile list's pixel p (k_pixel_map)
+            x = xy & 0xFFFFu; y = xy >> 16; s = pass;
         }
         uint32_t canonical = fp.frame_count + s;
         uint32_t tile = (y / fp.tile_h)*fp.tcx + (x / fp.tile_w);
@@ -1946,6 +1959,8 @@ struct rt_scene {
     Partition part[MAX_PARTITIONS];
     hipEvent_t start_ev = nullptr;
     uint32_t* d_tiles = nullptr;
+    uint32_t* d_pixmap = nullptr;   // FrameParams::pix_xy
+    size_t pixmap_cap = 0;
     size_t tiles_cap = 0;
     int32_t* d_tile_base = nullptr;
     size_t tile_base_cap = 0;
@@ -2483,9 +2498,12 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             if (M.indices[t] >= M.triangle_count) { set_error("mesh index out of range"); return fail(RT_ERROR_INVALID); }
             orig.push_back(M.indices[t]);
         }
+        // vertex normals gathered into BVH slot order (the reference looks them up by the
+        // original index, get_normals(mesh)[indices[slot]], RT/intersection.cpp:574-578):
+        // the hit's slot then addresses them directly
         for (uint32_t t = 0; t < M.triangle_count; ++t)
             for (int k = 0; k < 3; ++k) {
-                rt_v3 nn = meshes[m].has_normals ? M.normals[3*(size_t)t + k] : rt_v3{0, 0, 0};
+                rt_v3 nn = meshes[m].has_normals ? M.normals[3*(size_t)M.indices[t] + k] : rt_v3{0, 0, 0};
                 normals.push_back(nn.x); normals.push_back(nn.y); normals.push_back(nn.z);
             }
         mnodes.insert(mnodes.end(), M.nodes, M.nodes + M.node_count);
@@ -2612,6 +2630,7 @@ int rt_scene_free(rt_scene* s) {
     for (auto& pt : s->part) free_partition(pt);
     if (s->start_ev) (void)hipEventDestroy(s->start_ev);
     if (s->d_tiles) (void)hipFree(s->d_tiles);
+    if (s->d_pixmap) (void)hipFree(s->d_pixmap);
     if (s->d_tile_base) (void)hipFree(s->d_tile_base);
     if (s->d_samp) (void)hipFree(s->d_samp);
     if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
@@ -2709,6 +2728,16 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.tile_ids = s->d_tiles;
     fp.tile_prefix = s->d_tiles + ids.size();
     fp.pixels = prefix.back();
+    if (w > 65535 || h > 65535) { set_error("frame larger than 65535 pixels a side"); return RT_ERROR_INVALID; }
+    if (s->pixmap_cap < fp.pixels) {
+        if (s->d_pixmap) (void)hipFree(s->d_pixmap);
+        s->d_pixmap = nullptr; s->pixmap_cap = 0;
+        HIP_OK(hipMalloc(&s->d_pixmap, sizeof(uint32_t)*(size_t)fp.pixels));
+        s->pixmap_cap = fp.pixels;
+    }
+    k_pixel_map<<<fp.ntiles, 256, 0, stream>>>(fp, s->d_pixmap);
+    HIP_OK(hipGetLastError());
+    fp.pix_xy = s->d_pixmap;
     fill_camera(fp, camera);
     fp.lut = s->d_lut;
     fp.kernel_size = (int32_t)filter->kernel_size;
