@@ -1181,7 +1181,7 @@ RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return b
 // Kernels
 // ======================================================================
 constexpr int BLOCK = 512;          // slot-ordered kernels (generate / shade / splat)
-constexpr int EV_SLOTS = 4;     // iterations between host syncs in run_frame
+constexpr int EV_SLOTS = 8;     // iterations in flight per partition in run_frame (2 chunks of 4)
 
 // k_pixel_map — the coordinates of every pixel of the shard's tile list, in list
 // order (tiles descending, raster inside a tile: RT/raytracer.cpp:555, :409-410),
@@ -1943,7 +1943,8 @@ struct Partition {
     Pool pool = {};
     std::vector<void*> pool_allocs;
     Counters* cnt = nullptr;
-    Counters* cnt_host = nullptr;       // pinned
+    Counters* cnt_host = nullptr;       // pinned, [2]: the counters after chunk c land in [c % 2]
+    hipEvent_t chunk_done[2] = {};
     uint2* spill = nullptr;             // traversal stack levels beyond STACK_LDS
     hipStream_t own_stream = nullptr;   // partitions > 0 (partition 0 runs on the caller's stream)
     hipEvent_t join = nullptr;
@@ -2122,6 +2123,7 @@ void free_partition(Partition& pt) {
     if (pt.spill) (void)hipFree(pt.spill);
     if (pt.own_stream) (void)hipStreamDestroy(pt.own_stream);
     if (pt.join) (void)hipEventDestroy(pt.join);
+    for (auto& e : pt.chunk_done) if (e) (void)hipEventDestroy(e);
     if (pt.events) for (auto& e : pt.ev) (void)hipEventDestroy(e);
     pt = Partition{};
 }
@@ -2131,7 +2133,8 @@ int ensure_partition(rt_scene* s, int k) {
     Partition& pt = s->part[k];
     if (pt.cnt) return RT_OK;
     HIP_OK(hipMalloc(&pt.cnt, sizeof(Counters)));
-    HIP_OK(hipHostMalloc(&pt.cnt_host, sizeof(Counters)));
+    HIP_OK(hipHostMalloc(&pt.cnt_host, 2*sizeof(Counters)));
+    for (auto& e : pt.chunk_done) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipMalloc(&pt.spill, sizeof(uint2)*(size_t)(STACK_DEPTH - STACK_LDS)*s->trace_grid*TB));
     if (k > 0) HIP_OK(hipStreamCreateWithFlags(&pt.own_stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&pt.join, hipEventDisableTiming));
@@ -2205,7 +2208,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(s->start_ev, stream));
-    struct Run { hipStream_t stream; uint32_t grid; uint64_t iters; int cur; bool live; int pending[EV_SLOTS]; int npending; };
+    struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live; int final_buf;
+                 uint64_t chunk_first[2]; int chunk_n[2]; };
     Run run[MAX_PARTITIONS] = {};
     double kms[RT_KERNEL_COUNT] = {};
     uint64_t klaunch[RT_KERNEL_COUNT] = {};
@@ -2233,28 +2237,29 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         }
     }
     // Stage timing without extra host syncs: each iteration records begin/end
-    // events into one of EV_SLOTS ring slots; the slots are read back at the
-    // host sync points the loop already has (every 4 iterations).
+    // events into one of EV_SLOTS ring slots; a chunk's slots are read back when
+    // the host has waited for that chunk anyway.
     auto ev = [&](int k, int slot, int kern, int end) -> hipEvent_t& {
         return s->part[k].ev[(slot*RT_KERNEL_COUNT + kern)*2 + end];
     };
-    auto harvest = [&](int k) {
+    auto harvest = [&](int k, int b) {
         Run& r = run[k];
-        for (int i = 0; i < r.npending; ++i)
+        if (!prof) return;
+        for (int i = 0; i < r.chunk_n[b]; ++i) {
+            const int slot = (int)((r.chunk_first[b] + i) % EV_SLOTS);
             for (int kern = 0; kern < RT_KERNEL_COUNT - 1; ++kern) {
                 float ms = 0.0f;
-                if (hipEventElapsedTime(&ms, ev(k, r.pending[i], kern, 0), ev(k, r.pending[i], kern, 1)) == hipSuccess) {
+                if (hipEventElapsedTime(&ms, ev(k, slot, kern, 0), ev(k, slot, kern, 1)) == hipSuccess) {
                     kms[kern] += ms; klaunch[kern] += 1;
                 }
             }
-        r.npending = 0;
+        }
     };
     auto iterate = [&](int k) {
         Partition& pt = s->part[k];
         Run& r = run[k];
         const hipStream_t q = r.stream;
         const int slot = (int)(r.iters % EV_SLOTS);
-        if (prof) r.pending[r.npending++] = slot;
         auto b = [&](int kern) { if (prof) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
         auto e = [&](int kern) { if (prof) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
         b(RT_KERNEL_GENERATE);
@@ -2272,25 +2277,45 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         ++r.iters;
         r.cur ^= 1;
     };
+    // A chunk: 4 iterations (1 in a partition's first 3 chunks), then the counters into
+    // the pinned buffer of the chunk's parity and an event.  Every live partition keeps
+    // two chunks in flight, so while the host reads one chunk's counters the next one
+    // already runs and the partitions never drain between host checks.
+    auto enqueue_chunk = [&](int k) -> int {
+        Partition& pt = s->part[k];
+        Run& r = run[k];
+        const int b = (int)(r.chunks & 1);
+        r.chunk_first[b] = r.iters;
+        r.chunk_n[b] = r.chunks < 3 ? 1 : 4;
+        for (int i = 0; i < r.chunk_n[b]; ++i) iterate(k);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(pt.cnt_host + b, pt.cnt, sizeof(Counters), hipMemcpyDeviceToHost, r.stream));
+        HIP_OK(hipEventRecord(pt.chunk_done[b], r.stream));
+        ++r.chunks;
+        return RT_OK;
+    };
     s->cancel = 0;
+    for (int c = 0; c < 2; ++c)
+        for (int k = 0; k < nparts; ++k) {
+            int err = enqueue_chunk(k);
+            if (err) return err;
+        }
     uint64_t rounds = 0;
     for (int live = nparts; live > 0; ++rounds) {
-        // a round: 4 iterations of every live partition, interleaved (1 in the first 3 rounds),
-        // then each partition's counters come back for the termination test
-        const int per_round = rounds < 3 ? 1 : 4;
-        for (int i = 0; i < per_round; ++i)
-            for (int k = 0; k < nparts; ++k)
-                if (run[k].live) iterate(k);
-        HIP_OK(hipGetLastError());
-        for (int k = 0; k < nparts; ++k)
-            if (run[k].live)
-                HIP_OK(hipMemcpyAsync(s->part[k].cnt_host, s->part[k].cnt, sizeof(Counters), hipMemcpyDeviceToHost, run[k].stream));
         for (int k = 0; k < nparts; ++k) {
-            if (!run[k].live) continue;
-            HIP_OK(hipStreamSynchronize(run[k].stream));
-            harvest(k);
-            const Counters& c = *s->part[k].cnt_host;
-            if (c.next_sample >= c.total_samples && c.pending == 0) { run[k].live = false; --live; }
+            Run& r = run[k];
+            if (!r.live) continue;
+            const int b = (int)(r.consumed & 1);
+            HIP_OK(hipEventSynchronize(s->part[k].chunk_done[b]));
+            harvest(k, b);
+            ++r.consumed;
+            const Counters& c = s->part[k].cnt_host[b];
+            if (c.next_sample >= c.total_samples && c.pending == 0) {
+                r.live = false; r.final_buf = b; --live;       // its chunk still in flight finds nothing to do
+            } else {
+                int err = enqueue_chunk(k);
+                if (err) return err;
+            }
         }
         if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
         if (rounds > 100000) { set_error("wavefront loop did not converge"); return RT_ERROR_DEVICE; }
@@ -2302,7 +2327,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     Counters sum = {};
     uint64_t iters = 0;
     for (int k = 0; k < nparts; ++k) {
-        const Counters& c = *s->part[k].cnt_host;
+        const Counters& c = s->part[k].cnt_host[run[k].final_buf];
         sum.closest_rays += c.closest_rays;
         sum.shadow_rays += c.shadow_rays;
         sum.traced_rays[0] += c.traced_rays[0];
