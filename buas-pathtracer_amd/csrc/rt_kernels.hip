@@ -1201,12 +1201,20 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     __shared__ uint32_t agg[BLOCK / 64 + 1];
     __shared__ float4 lds_scene[LDS_SCENE_Q];
     const DevScene sc = scene_in_lds(sc_g, lds_scene);
-    const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
-    const bool want = slot < pool.n && pool.state[slot] == S_FREE;
-    // free slots claim consecutive sample numbers in slot order: the block's first
-    // claim is the scan of the free counts k_bookkeep made (no atomics)
+    // Free slots claim consecutive sample numbers in slot order: the block's first
+    // claim is the scan of the free counts k_bookkeep made (no atomics).  The block's
+    // free slots are handed to its first nfree threads (slot order kept), so the waves
+    // past them skip the ray setup entirely (about 2/3 of the pool is busy at any time).
+    __shared__ uint16_t freelist[BLOCK];
+    const uint32_t own = blockIdx.x*blockDim.x + threadIdx.x;
+    const bool own_free = own < pool.n && pool.state[own] == S_FREE;
     uint32_t nfree;
-    const uint32_t claim = pool.claim_base[blockIdx.x] + block_rank<BLOCK>(want, agg, &nfree);
+    const uint32_t rank = block_rank<BLOCK>(own_free, agg, &nfree);
+    if (own_free) freelist[rank] = (uint16_t)threadIdx.x;
+    __syncthreads();
+    const bool want = threadIdx.x < nfree;
+    const uint32_t slot = blockIdx.x*blockDim.x + (want ? (uint32_t)freelist[threadIdx.x] : threadIdx.x);
+    const uint32_t claim = pool.claim_base[blockIdx.x] + threadIdx.x;
     const bool active = want && (unsigned long long)claim < remaining_samples(cnt);
     bool enqueue = false, cast = false;
     V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
