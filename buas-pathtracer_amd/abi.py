@@ -169,6 +169,10 @@ ABI_FUNCTIONS = {
                                    C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, P(C.c_uint32), P(C.c_uint32),
                                    P(C.c_float), P(Stats)]),
     "rt_debug_intersect": (C.c_int, [C.c_void_p, C.c_uint32, P(RayQuery), C.c_int, P(HitRecord)]),
+    "rt_debug_mesh_bvh4": (C.c_int, [P(BvhNode), C.c_uint32, P(C.c_float), C.c_uint32, P(C.c_uint32),
+                                     P(C.c_uint32)]),
+    "rt_debug_top_sequences": (C.c_int, [P(BvhNode), C.c_uint32, C.c_uint32, P(C.c_float), C.c_uint32,
+                                         P(C.c_uint32)]),
     "rt_set_profiling": (C.c_int, [C.c_int]),
     "rt_set_path_pool": (C.c_int, [C.c_uint32]),
     "rt_cancel": (C.c_int, [C.c_void_p]),

@@ -2878,6 +2878,36 @@ int rt_trace_samples(rt_scene* s, const rt_camera* camera, const rt_settings* st
     return err;
 }
 
+int rt_debug_mesh_bvh4(const rt_bvh_node* nodes, uint32_t node_count, float* out, uint32_t out_cap_nodes,
+                       uint32_t* out_nodes, uint32_t* out_root_record) {
+    if (!nodes || !node_count || !out_nodes || !out_root_record) { set_error("null argument"); return RT_ERROR_INVALID; }
+    std::vector<float4> q;
+    uint32_t root;
+    if (nodes[0].count) {
+        root = pack_node(0u, nodes[0].left_first, nodes[0].count, 0u);
+    } else {
+        bool ok = true;
+        uint32_t need = 0;
+        root = build_bvh4(nodes, node_count, 0u, 0u, q, need, ok);
+        if (!ok) { set_error("BVH too large for the BVH4 records"); return RT_ERROR_INVALID; }
+    }
+    *out_nodes = (uint32_t)(q.size() / 8);
+    *out_root_record = root;
+    if (out && out_cap_nodes >= *out_nodes) memcpy(out, q.data(), q.size()*sizeof(float4));
+    return (out && out_cap_nodes < *out_nodes) ? RT_ERROR_INVALID : RT_OK;
+}
+
+int rt_debug_top_sequences(const rt_bvh_node* nodes, uint32_t node_count, uint32_t index_count,
+                           float* out, uint32_t out_cap_entries, uint32_t* out_len) {
+    if (!nodes || !out_len) { set_error("null argument"); return RT_ERROR_INVALID; }
+    uint32_t len = 0;
+    std::vector<float4> q = top_sequences(nodes, node_count, index_count, len);
+    *out_len = len;
+    if (q.empty()) { set_error("top level too large for the prologue"); return RT_ERROR_INVALID; }
+    if (out && out_cap_entries >= 8*len) memcpy(out, q.data(), q.size()*sizeof(float4));
+    return (out && out_cap_entries < 8*len) ? RT_ERROR_INVALID : RT_OK;
+}
+
 int rt_debug_intersect(rt_scene* s, uint32_t count, const rt_ray_query* rays, int occlusion, rt_hit_record* out) {
     if (!s || !rays || !out) { set_error("null argument"); return RT_ERROR_INVALID; }
     if (!count) return RT_OK;

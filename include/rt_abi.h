@@ -280,6 +280,21 @@ int rt_trace_samples(rt_scene* scene, const rt_camera* camera, const rt_settings
 int rt_debug_intersect(rt_scene* scene, uint32_t count, const rt_ray_query* rays,
                        int occlusion, rt_hit_record* out);
 
+/* Verification entries for the device layouts built at rt_scene_upload (host only,
+ * no device needed).  rt_debug_mesh_bvh4: the BVH4 a mesh BVH2 (the caller's
+ * BVHNode array, RT/bvh.h:31-37) is traversed as, 8 x float4 per node (SoA
+ * children: p.x[4] p.y[4] p.z[4] r.x[4] r.y[4] r.z[4], packed records[4], split
+ * axes); interior records are node indices, leaf records bit 30 | count << 25 |
+ * first, 0xFFFFFFFF no child.  rt_debug_top_sequences: the top level as the ray
+ * prologue walks it, per direction octant (bit k = d[k] < 0) node_count entries of
+ * 2 x float4 {bv_p, bv_r.x}, {bv_r.yz, leaf info (0x80000000 | count << 24 | first,
+ * 0 interior), skip (the entry after the subtree)}.  Both return RT_ERROR_INVALID
+ * when the tree does not fit the layout, and write the counts they need. */
+int rt_debug_mesh_bvh4(const rt_bvh_node* nodes, uint32_t node_count, float* out, uint32_t out_cap_nodes,
+                       uint32_t* out_nodes, uint32_t* out_root_record);
+int rt_debug_top_sequences(const rt_bvh_node* nodes, uint32_t node_count, uint32_t index_count,
+                           float* out, uint32_t out_cap_entries, uint32_t* out_len);
+
 /* The output pass of RT/raytracer.cpp:2103-2171 on the device: per pixel resolve
  * (xyz / w), exposure, 1-exp(-x) tonemap, sRGB power, sigmoidal contrast, x255,
  * TPDF dither from the reference's LDR_RGB1 blue-noise texture number
