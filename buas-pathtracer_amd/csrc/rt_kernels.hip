@@ -67,6 +67,7 @@ struct DevScene {
     const float4* top_seq;          // top level in the ray prologue: [8 octants][top_seq_len] x 2 float4, or null
     uint32_t top_seq_len;
     uint32_t mlist_max;             // mesh-list capacity, <= MLIST_MAX (RT_MLIST_MAX lowers it for tests)
+    uint32_t listed_only;           // top_seq and no more mesh slots than mlist_max: no ray is MLIST_FULL
     uint32_t finite_boxes;          // every node box within 2^40 of the origin (finite_box_ray)
     const uint32_t* bvh_idx;
     const float4* leaf_rec;         // [bvh_index_count][LEAF_REC_Q]: everything a top-level leaf step needs
@@ -521,7 +522,7 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
     return r;
 }
 
-template <bool OCC>
+template <bool OCC, bool LST = false>
 struct Traversal {
     V3 wo, wd;          // world ray
     V3 co, cd, cinv;    // current ray (object space while in a mesh)
@@ -681,8 +682,11 @@ struct Traversal {
             mode = TM_LEAF;                                        // instance finished
             set_world();
         }
-        if (mode == TM_LEAF && leaf_cur == leaf_end) mode = TM_TOP;
-        if (mode == TM_TOP) {
+        if (mode == TM_LEAF && leaf_cur == leaf_end) {
+            if (LST) { mode = TM_DONE; return false; }             // the mesh list is the whole walk
+            mode = TM_TOP;
+        }
+        if (!LST && mode == TM_TOP) {
             if (!has_cur && !pop<SH>(st, sc.bvh_src, 0)) { mode = TM_DONE; return false; }
             if (cur_cnt) {                                         // top-level leaf: its primitives in order
                 leaf_cur = cur_lf; leaf_end = cur_lf + cur_cnt; has_cur = false;
@@ -694,14 +698,14 @@ struct Traversal {
         uint32_t nq;
         if (mode == TM_LEAF) {
             RT_STAT(6);
-            src = sc.leaf_rec + (size_t)(listed ? (leaf_list & 63u) : leaf_cur)*LEAF_REC_Q; nq = LEAF_REC_Q;
+            src = sc.leaf_rec + (size_t)((LST || listed) ? (leaf_list & 63u) : leaf_cur)*LEAF_REC_Q; nq = LEAF_REC_Q;
         } else if (cur_cnt) {                                      // mesh leaf
             RT_STAT(5);
             src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
         } else {                                                   // interior: the sibling pair
             RT_STAT(4);
 #if RT_MESH_BVH4
-            if (mode == TM_MESH) { src = sc.mnodes4 + 8*(size_t)cur_lf; nq = 8; }
+            if (LST || mode == TM_MESH) { src = sc.mnodes4 + 8*(size_t)cur_lf; nq = 8; }
             else
 #endif
             { src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4; }
@@ -759,7 +763,7 @@ struct Traversal {
             return true;
         }
 #if RT_MESH_BVH4
-        if (mode == TM_MESH) push_children4<SH, FIN>(st, F);
+        if (LST || mode == TM_MESH) push_children4<SH, FIN>(st, F);
         else
 #endif
         push_children<SH, FIN>(st, F);
@@ -1313,7 +1317,10 @@ constexpr int STEPS_PER_REFILL = RT_STEPS_PER_REFILL;
 #define RT_TRACE_WAVES 4
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
-template <bool OCC>
+// LST: every queued ray carries a mesh list (the scene's top level is walked in the
+// prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
+// the kernel is built without the top-level walk.
+template <bool OCC, bool LST>
 __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag) {
     __shared__ uint2 lds_stack[STACK_LDS*TB];
     Stack st;
@@ -1331,7 +1338,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     bool exhausted = false, active = false;
     uint32_t item = 0;
     uint32_t steps = 0;
-    Traversal<OCC> tr;
+    Traversal<OCC, LST> tr;
     auto finish = [&]() {
         if (diag) {                                   // RT_DEBUG_TRAVERSAL: longest traversals
             atomicMax(&cnt->max_steps[OCC ? 1 : 0], steps);
@@ -2273,11 +2280,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         b(RT_KERNEL_GENERATE);
         k_generate<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
-        k_trace<false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         k_shade<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        k_trace<true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_CONNECT); b(RT_KERNEL_SPLAT);
         k_splat<<<r.grid, BLOCK, 0, q>>>(fp, pt.pool, pt.cnt);
         e(RT_KERNEL_SPLAT);
@@ -2484,6 +2493,10 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             if ((err = upload(s, seq.data(), seq.size(), &ds.top_seq))) return fail(err);
             ds.top_seq_len = len;
         }
+        uint32_t mesh_slots = 0;
+        for (uint32_t j = 0; j < d->bvh_index_count; ++j)
+            mesh_slots += d->primitives[d->bvh_indices[j]].type == RT_PRIMITIVE_MESH ? 1u : 0u;
+        ds.listed_only = (ds.top_seq && mesh_slots <= ds.mlist_max) ? 1u : 0u;
     }
     ds.bvh_node_count = d->bvh_node_count;
     // meshes: concatenate, triangles as (a, b-a, c-a) float4 triples
@@ -2647,7 +2660,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("hipGetDeviceProperties"); return fail(RT_ERROR_DEVICE); }
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);

@@ -15,9 +15,9 @@ import glob
 import json
 import os
 
-KERNELS = ["k_generate", "k_trace<false>", "k_shade", "k_trace<true>", "k_splat", "k_resolve", "k_bookkeep"]
-LABEL = {"k_trace<false>": "k_extend (k_trace<false>)", "k_trace<true>": "k_connect (k_trace<true>)"}
-KEYS = {"k_trace<false>": "k_extend", "k_trace<true>": "k_connect"}
+KERNELS = ["k_generate", "k_trace<false", "k_shade", "k_trace<true", "k_splat", "k_resolve", "k_bookkeep"]
+LABEL = {"k_trace<false": "k_extend (k_trace<false, .>)", "k_trace<true": "k_connect (k_trace<true, .>)"}
+KEYS = {"k_trace<false": "k_extend", "k_trace<true": "k_connect"}
 
 
 def short(name):
