@@ -124,6 +124,9 @@ def main():
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0, help="in-flight path pool size (0 = default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard-of", type=int, default=0,
+                    help="diagnostic (1 process): render only rank 0's tiles of an N-rank frame, to size the "
+                         "per-rank work of the N-GPU strong-scaling run; not a bench line")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
@@ -169,6 +172,8 @@ def main():
 
     def step():
         accum.zero_()
+        if args.shard_of > 1:                          # diagnostic: rank 0's share of an N-rank frame
+            return render_shard(0, args.shard_of, accum)
         # tiles t % world == rank, then the RCCL sum-reduce of the framebuffer over xGMI
         return render_frame_sharded(render_shard, accum, rank, world)
 
@@ -282,7 +287,7 @@ def main():
             "config": {"workload": f"{args.config}: {cfg['preset']} {w}x{h} {st.samples_per_pixel}spp "
                                    f"depth {st.max_bounce_count}", "width": w, "height": h,
                        "spp": st.samples_per_pixel, "max_depth": st.max_bounce_count,
-                       "parallelism": f"tiles%{world}" + ("+rccl_reduce" if world > 1 else "")},
+                       "parallelism": (f"tiles%{args.shard_of} (rank 0 only, diagnostic)" if args.shard_of > 1 else f"tiles%{world}" + ("+rccl_reduce" if world > 1 else ""))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": KERNEL[dom], "bytes_per_unit": BYTES_PER_UNIT[dom],
