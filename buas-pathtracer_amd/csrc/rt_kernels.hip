@@ -1717,6 +1717,10 @@ __global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Coun
 #define RT_RES_RY 4
 #endif
 constexpr int RES_RY = RT_RES_RY;      // 4: measured best of 2, 4, 6, 8, 16 (C3 256 spp: 30 ms)
+#ifndef RT_RES_U
+#define RT_RES_U 8
+#endif
+constexpr int RES_U = RT_RES_U;        // sample records loaded ahead per thread
 constexpr int RES_BX = 64, RES_BY = 4;
 __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
     __shared__ float lut[512];
@@ -1752,10 +1756,7 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
                     const size_t p = (size_t)base + (size_t)(y - min_y)*twid + (size_t)(x - min_x);
                     if (ks) {
                         const float fdx = dx - (float)x;
-                        for (uint32_t s = 0; s < fp.spp; ++s) {
-                            const size_t rr = (size_t)s*P + p;
-                            const float4 c = fp.samp_rgbx[rr];
-                            const float jy = fp.samp_jy[rr];
+                        auto splat = [&](const float4 c, const float jy) {
                             const float fx = lut[(int)fabsf(0.5f + kscale*(fdx - c.w))];
 #pragma unroll
                             for (int r = 0; r < RES_RY; ++r) {
@@ -1768,6 +1769,25 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
                                 acc[r].z = acc[r].z + f*c.z;
                                 acc[r].w = acc[r].w + f;
                             }
+                        };
+                        // RES_U records in flight per thread: with few waves (a shard's frame)
+                        // one load at a time would expose the full memory latency per sample
+                        uint32_t s = 0;
+                        for (; s + RES_U <= fp.spp; s += RES_U) {
+                            float4 c[RES_U];
+                            float jy[RES_U];
+#pragma unroll
+                            for (int u = 0; u < RES_U; ++u) {
+                                const size_t rr = (size_t)(s + u)*P + p;
+                                c[u] = fp.samp_rgbx[rr];
+                                jy[u] = fp.samp_jy[rr];
+                            }
+#pragma unroll
+                            for (int u = 0; u < RES_U; ++u) splat(c[u], jy[u]);
+                        }
+                        for (; s < fp.spp; ++s) {
+                            const size_t rr = (size_t)s*P + p;
+                            splat(fp.samp_rgbx[rr], fp.samp_jy[rr]);
                         }
                     } else {                                   // box filter: the pixel's own samples, (result, 1)
                         const int r = y - Y0;
