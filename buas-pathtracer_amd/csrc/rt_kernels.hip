@@ -2811,20 +2811,33 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.accum = reinterpret_cast<float4*>(d_pixels);
     unsigned long long total = (unsigned long long)fp.pixels*st->samples_per_pixel;
     if (total == 0) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
-    // Deterministic splat (k_resolve) needs spp*P 20-byte sample records in HBM;
-    // above the budget the frame falls back to float-atomic splats.
-    const char* bud = getenv("RT_SAMPLE_BUDGET_GB");
-    const double budget = (bud ? atof(bud) : 96.0)*1e9;
-    const bool gather = (double)total*20.0 <= budget;
-    if (gather) {
-        if (s->samp_cap < total) {
+    // Deterministic splat (k_resolve) needs spp*P 20-byte sample records in HBM.  The
+    // budget is the device's free memory (plus the records already held) less 16 GB for
+    // the partitions' path pools; above it the frame falls back to float-atomic splats.
+    double budget;
+    if (const char* bud = getenv("RT_SAMPLE_BUDGET_GB")) {
+        budget = atof(bud)*1e9;
+    } else {
+        size_t free_b = 0, total_b = 0;
+        HIP_OK(hipMemGetInfo(&free_b, &total_b));
+        budget = (double)free_b + 20.0*(double)s->samp_cap - 16e9;
+    }
+    bool gather = (double)total*20.0 <= budget;
+    if (gather && s->samp_cap < total) {
+        if (s->d_samp) (void)hipFree(s->d_samp);
+        if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
+        s->d_samp = nullptr; s->d_samp_jy = nullptr; s->samp_cap = 0;
+        if (hipMalloc(&s->d_samp, sizeof(float4)*total) != hipSuccess ||
+            hipMalloc(&s->d_samp_jy, sizeof(float)*total) != hipSuccess) {
+            (void)hipGetLastError();
             if (s->d_samp) (void)hipFree(s->d_samp);
-            if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
-            s->d_samp = nullptr; s->d_samp_jy = nullptr; s->samp_cap = 0;
-            HIP_OK(hipMalloc(&s->d_samp, sizeof(float4)*total));
-            HIP_OK(hipMalloc(&s->d_samp_jy, sizeof(float)*total));
+            s->d_samp = nullptr; s->d_samp_jy = nullptr;
+            gather = false;                                   // out of memory: atomic splat
+        } else {
             s->samp_cap = total;
         }
+    }
+    if (gather) {
         const size_t ntile_all = (size_t)fp.tcx*tcy;
         std::vector<int32_t> base(ntile_all, -1);
         for (size_t i = 0; i < ids.size(); ++i) base[ids[i]] = (int32_t)prefix[i];

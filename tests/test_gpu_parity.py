@@ -295,3 +295,19 @@ def test_top_level_paths(rt, env, monkeypatch):
     REPORT["top_level_" + "_".join(f"{k}={v}" for k, v in env.items())] = {"bit_exact_fraction": float(same)}
     assert same >= 0.999
     assert gstats.closest_hit_rays == cstats.closest_hit_rays or same < 1.0
+
+
+def test_atomic_splat_fallback(rt, monkeypatch):
+    """Frames whose sample records exceed the HBM budget splat with float atomics
+    (k_splat): the same image up to float summation order."""
+    monkeypatch.setenv("RT_SAMPLE_BUDGET_GB", "0")
+    scene, cam, st, fc, post = rt.load_preset("c1", 128, 128)
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        gpu, stats = dev.render(cam, st, fc, 128, 128)
+    finally:
+        dev.close()
+    cpu, cstats = ob.render(scene.desc(), cam, st, fc, 128, 128, rng_mode=0, threads=8)
+    REPORT["atomic_splat_c1_128"] = {"rel_l2": rel_l2(gpu, cpu)}
+    assert (stats.closest_hit_rays, stats.shadow_rays) == (cstats.closest_hit_rays, cstats.shadow_rays)
+    assert rel_l2(gpu, cpu) <= 1e-5
