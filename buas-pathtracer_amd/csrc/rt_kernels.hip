@@ -1309,7 +1309,11 @@ constexpr uint32_t CHUNK = 256;
 #ifndef RT_STEPS_PER_REFILL
 #define RT_STEPS_PER_REFILL 8
 #endif
+#ifndef RT_STEPS_PER_REFILL_SHADOW
+#define RT_STEPS_PER_REFILL_SHADOW RT_STEPS_PER_REFILL
+#endif
 constexpr int STEPS_PER_REFILL = RT_STEPS_PER_REFILL;
+constexpr int STEPS_PER_REFILL_SHADOW = RT_STEPS_PER_REFILL_SHADOW;
 
 // 4 waves per SIMD (128 VGPRs): the BVH4 step wants ~138, i.e. 3 waves; the few
 // spilled values cost less than the lost occupancy (C3: 5446 vs 5389 Mrays/s)
@@ -1407,10 +1411,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
         }
         if (__ballot(active) == 0ull) break;
 #ifdef RT_STEP_STATS
-        if (lane == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) tr.stat[1] += 64*STEPS_PER_REFILL;
+        if (lane == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) tr.stat[1] += 64*(OCC ? STEPS_PER_REFILL_SHADOW : STEPS_PER_REFILL);
 #endif
         if (active) {
-            for (int k = 0; k < STEPS_PER_REFILL; ++k) {
+            for (int k = 0; k < (OCC ? STEPS_PER_REFILL_SHADOW : STEPS_PER_REFILL); ++k) {
                 ++steps;
                 if (!tr.step(sc, st)) { finish(); active = false; break; }
             }
