@@ -177,11 +177,21 @@ def main():
         # tiles t % world == rank, then the RCCL sum-reduce of the framebuffer over xGMI
         return render_frame_sharded(render_shard, accum, rank, world)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(device)
-
+    # Warm-up frames time every stage (HIP events around each launch); the timed region
+    # then records events for the dominant stage only, since each event pair is a queue
+    # marker that costs the other launches ~0.5 % of the frame (2.4 % for all stages).
     rt.lib().rt_set_profiling(1)
+    wms = [0.0] * 6
+    for _ in range(args.warmup):
+        s = step()
+        for k in range(6):
+            wms[k] += s.kernel_ms[k] / args.warmup
+    torch.cuda.synchronize(device)
+    if args.warmup:
+        dom_stage = max(range(5), key=lambda k: wms[k])
+        rt.lib().rt_set_profiling_stages(1 << dom_stage)
+    if os.environ.get("RT_BENCH_NO_STAGE_EVENTS"):
+        rt.lib().rt_set_profiling(0)
     closest = shadow = samples = traced = traced_sh = 0
     kms = [0.0] * 6
     kl = [0] * 6
@@ -223,7 +233,7 @@ def main():
         # kernels ran at once on average, and `isolated` gives the serialized figures
         # (rocprofv3 --pmc runs, profiles/traffic.json) for the same kernel.
         units = {"generate": samples, "extend": traced, "shade": closest, "connect": traced_sh, "splat": samples}
-        dom = max(BYTES_PER_UNIT, key=lambda k: kms[STAGES.index(k)])
+        dom = max(BYTES_PER_UNIT, key=lambda k: kms[STAGES.index(k)])     # the only stage timed (warm-up > 0)
         di = STAGES.index(dom)
         mean_launch_s = (kms[di] / 1e3) / max(kl[di], 1)
         units_per_launch = units[dom] / max(kl[di], 1)
@@ -241,7 +251,8 @@ def main():
                             "frac": round(iso_gbs / HBM_PEAK_GBS, 4), "source": tj.get("source")}
         except (OSError, ValueError, KeyError):
             pass
-        concurrency = sum(kms[:5]) / (elapsed * 1e3) if elapsed > 0 else 0.0
+        ref = wms if args.warmup else [x / args.steps for x in kms]        # all stages: warm-up frames
+        concurrency = sum(ref[:5]) / (elapsed * 1e3 / args.steps) if elapsed > 0 else 0.0
         pipe_bytes = PIPE_BYTES_PER_RAY * (closest + shadow) + PIPE_BYTES_PER_SAMPLE * samples
         pipe_gbs = pipe_bytes / elapsed / 1e9
         # output pass on the resolved frame: k_post, 16 B read + 4 B written per pixel
@@ -297,8 +308,10 @@ def main():
                          "pipeline": {"bytes": pipe_bytes, "achieved": round(pipe_gbs, 1),
                                       "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
                                       "formula": "152 B x (closest + shadow rays) + 144 B x samples, rank 0, / wall time"}},
-            "stage_ms_per_step": {n: round(kms[i] / args.steps, 2) for i, n in
-                                  enumerate(["generate", "extend", "shade", "connect", "splat", "resolve"])},
+            "stage_ms_per_step": {n: round((wms[i] if args.warmup else kms[i] / args.steps), 2) for i, n in
+                                  enumerate(STAGES)},
+            "stage_ms_note": ("HIP-event time per stage summed over its launches, from the warm-up frames "
+                              "(4 partitions overlap, so the sum exceeds ms_per_step)"),
             "cpu_baseline": cpu,
             "postprocess": postprocess,
         }

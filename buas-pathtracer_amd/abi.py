@@ -174,6 +174,7 @@ ABI_FUNCTIONS = {
     "rt_debug_top_sequences": (C.c_int, [P(BvhNode), C.c_uint32, C.c_uint32, P(C.c_float), C.c_uint32,
                                          P(C.c_uint32)]),
     "rt_set_profiling": (C.c_int, [C.c_int]),
+    "rt_set_profiling_stages": (C.c_int, [C.c_uint32]),
     "rt_set_path_pool": (C.c_int, [C.c_uint32]),
     "rt_cancel": (C.c_int, [C.c_void_p]),
     "rt_postprocess_device": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, P(PostSettings), C.c_uint32,

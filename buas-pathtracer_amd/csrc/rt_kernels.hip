@@ -36,7 +36,7 @@ using namespace rtd;
 namespace {
 thread_local std::string g_error;
 void set_error(const std::string& s) { g_error = s; }
-bool g_profiling = false;
+uint32_t g_profiling = 0;       // stage mask: bit k = rt_kernel_stage k timed with HIP events
 uint32_t g_pool_override = 0;
 }
 
@@ -2243,7 +2243,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     if ((unsigned long long)pool_n*nparts > total) nparts = 1;
     if ((unsigned long long)pool_n > total) pool_n = (uint32_t)std::max<unsigned long long>(total, 1ull);
     pool_n = (pool_n + BLOCK - 1) / BLOCK * BLOCK;
-    const bool prof = g_profiling;
+    const uint32_t prof = g_profiling;
     const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(s->start_ev, stream));
@@ -2287,6 +2287,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         for (int i = 0; i < r.chunk_n[b]; ++i) {
             const int slot = (int)((r.chunk_first[b] + i) % EV_SLOTS);
             for (int kern = 0; kern < RT_KERNEL_COUNT - 1; ++kern) {
+                if (!((prof >> kern) & 1u)) continue;
                 float ms = 0.0f;
                 if (hipEventElapsedTime(&ms, ev(k, slot, kern, 0), ev(k, slot, kern, 1)) == hipSuccess) {
                     kms[kern] += ms; klaunch[kern] += 1;
@@ -2299,8 +2300,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         Run& r = run[k];
         const hipStream_t q = r.stream;
         const int slot = (int)(r.iters % EV_SLOTS);
-        auto b = [&](int kern) { if (prof) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
-        auto e = [&](int kern) { if (prof) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
+        auto b = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
+        auto e = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
         b(RT_KERNEL_GENERATE);
         k_generate<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
@@ -2445,7 +2446,8 @@ int rt_device_count(int* out) {
     return RT_OK;
 }
 
-int rt_set_profiling(int enable) { g_profiling = enable != 0; return RT_OK; }
+int rt_set_profiling(int enable) { g_profiling = enable ? (1u << RT_KERNEL_COUNT) - 1u : 0u; return RT_OK; }
+int rt_set_profiling_stages(uint32_t mask) { g_profiling = mask & ((1u << RT_KERNEL_COUNT) - 1u); return RT_OK; }
 int rt_set_path_pool(uint32_t paths) { g_pool_override = paths; return RT_OK; }
 
 int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
@@ -2862,15 +2864,16 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     if (err || !gather) return err;
     auto t0 = std::chrono::steady_clock::now();
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (g_profiling) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
+    const bool prof_resolve = (g_profiling >> RT_KERNEL_RESOLVE) & 1u;
+    if (prof_resolve) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
     dim3 rgrid((w + RES_BX - 1) / RES_BX, (h + RES_BY*RES_RY - 1) / (RES_BY*RES_RY));
     k_resolve<<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
     HIP_OK(hipGetLastError());
-    if (g_profiling) HIP_OK(hipEventRecord(e1, stream));
+    if (prof_resolve) HIP_OK(hipEventRecord(e1, stream));
     HIP_OK(hipStreamSynchronize(stream));
     if (stats) {
         stats->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        if (g_profiling) {
+        if (prof_resolve) {
             float ms = 0.0f;
             (void)hipEventElapsedTime(&ms, e0, e1);
             stats->kernel_ms[RT_KERNEL_RESOLVE] += ms;

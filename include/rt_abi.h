@@ -313,6 +313,9 @@ int rt_postprocess(int device, const rt_accumulation_buffer* accum, const rt_pos
 
 /* Record per-stage HIP-event timings into rt_stats::kernel_ms (off by default). */
 int rt_set_profiling(int enable);
+/* The same for a subset of stages: bit k = stage k of rt_kernel_stage (other stages
+ * record no events, so their launches are not slowed by the markers). */
+int rt_set_profiling_stages(uint32_t mask);
 
 /* Size of the in-flight path pool (paths resident in HBM); 0 = default (2^21). */
 int rt_set_path_pool(uint32_t paths);
