@@ -1,17 +1,18 @@
 // rt_kernels.hip — gfx950 wavefront path tracer: kernels + the rt_abi.h C ABI.
 //
 // Reference hot path (RT/ = /root/reference/Raytracer/):
-//   render_tile            RT/raytracer.cpp:366-495   -> k_generate + k_splat
+//   render_tile            RT/raytracer.cpp:366-495   -> k_generate (ray setup; splat of finished paths)
 //   advanced_integrator    RT/integrators.cpp:581-821 -> k_shade (one bounce per launch)
 //   intersect_scene        RT/intersection.cpp:606    -> k_extend
 //   intersect_shadow_ray   RT/intersection.cpp:600    -> k_connect
 //   samplers / RNG         RT/samplers.{h,cpp}        -> rt_dmath.h + sample_1d/2d below
-//   splat_filter           RT/raytracer.cpp:187-259   -> k_splat (float atomics)
+//   splat_filter           RT/raytracer.cpp:187-259   -> splat_sample records + k_resolve
 //
 // Wavefront loop: a pool of N in-flight paths lives in HBM as
 // structure-of-arrays with a state byte per slot.  One iteration = generate ->
-// extend -> shade -> connect -> splat -> bookkeep, each a separate kernel.
-// generate / shade / splat walk the pool in slot order; the two tracers
+// extend -> shade -> connect -> bookkeep, each a separate kernel (generate first
+// splats the paths the previous iteration finished).
+// generate / shade walk the pool in slot order; the two tracers
 // consume compacted queues (extension rays, shadow rays) that those kernels
 // append to with wave-aggregated atomics (__ballot + popcount + one atomic per
 // wavefront).  Paths are regenerated into freed slots every iteration so the
@@ -1008,7 +1009,7 @@ struct Pool {
     float4*   sh_rec;    // shadow queue, REC_Q float4 per ray: {o, light id}, {d, max_t}, {1/d, -}
     float4*   sh_c;      // contribution.xyz
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
-    uint32_t* free_n;    // [blocks]: free slots per BLOCK-slot block after k_splat
+    uint32_t* free_n;    // [blocks]: slots per BLOCK-slot block free for the next k_generate (k_shade)
     uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
 };
 
@@ -1029,8 +1030,10 @@ struct Counters {
     uint32_t fetch[2][NSHARD][LINE_WORDS];       // persistent trace kernels: items handed out (extend, connect)
     uint32_t cast[2][NSHARD][LINE_WORDS];        // rays cast this iteration: [0] new paths (k_generate), [1] shadow
     uint32_t alive[NSHARD][LINE_WORDS];          // paths k_shade continued (each casts a closest ray next iteration)
+    uint32_t unsplat[NSHARD][LINE_WORDS];        // paths finished this iteration, splatted by the next k_generate
     uint32_t gen_free;              // free slots counted by the last k_bookkeep = claims of the next k_generate
     uint32_t pending;               // paths queued for the next iteration (host termination test)
+    uint32_t pending_splat;         // finished paths the next k_generate splats (host termination test)
     uint32_t cancel;
     uint32_t pad;
     unsigned long long step_stats[2][8];   // RT_STEP_STATS builds: see k_trace
@@ -1187,6 +1190,60 @@ RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return b
 constexpr int BLOCK = 512;          // slot-ordered kernels (generate / shade / splat)
 constexpr int EV_SLOTS = 8;     // iterations in flight per partition in run_frame (2 chunks of 4)
 
+// The splat of a finished path (RT/raytracer.cpp:469-488): vignette, then the
+// 20-byte sample record k_resolve gathers (splat_filter :187-259 in reference
+// order), or float atomics into the accumulator when the records do not fit.
+// Run by k_generate on the slots the previous iteration finished, before it
+// reuses them.
+RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
+    {
+        const float4 L = pool.L[slot];
+        const float vig = pool.thr[slot].w;
+        const float2 j = pool.jitter[slot];
+        V3 r = muls(ld3(L), vig);
+        const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
+        if (fp.list_xy) {
+            const uint32_t k = __float_as_uint(pool.ray_d[slot].w);
+            float* o = fp.list_out + 5*(size_t)k;
+            o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = j.x; o[4] = j.y;
+        } else if (fp.samp_rgbx) {
+            // deterministic path: store the sample; k_resolve gathers it in reference order
+            const size_t rec = (size_t)__float_as_uint(pool.ray_d[slot].w)*fp.pixels + __float_as_uint(pool.prev_n[slot].w);
+            fp.samp_rgbx[rec] = make_float4(r.x, r.y, r.z, j.x);
+            fp.samp_jy[rec] = j.y;
+        } else if (fp.cache_size) {
+            const int64_t x = pixel % fp.w, y = pixel / fp.w;
+            const int64_t ks = fp.kernel_size;
+            const float kscale = (float)(fp.cache_size - 1) / (float)ks;
+            int64_t x0 = x - ks, x1 = x + ks + 1, y0 = y - ks, y1 = y + ks + 1;
+            int64_t xm = 0, ym = 0;
+            if (x0 < 0) { xm = -x0; x0 = 0; }
+            if (y0 < 0) { ym = -y0; y0 = 0; }
+            if (x1 > (int64_t)fp.w) x1 = fp.w;
+            if (y1 > (int64_t)fp.h) y1 = fp.h;
+            for (int64_t sy = y0; sy < y1; ++sy) {
+                int32_t jy = (int32_t)fabsf(0.5f + kscale*((float)(ym + (sy - y0) - ks) - j.y));
+                float fy = fp.lut[jy];
+                for (int64_t sx = x0; sx < x1; ++sx) {
+                    int32_t jx = (int32_t)fabsf(0.5f + kscale*((float)(xm + (sx - x0) - ks) - j.x));
+                    float f = fp.lut[jx]*fy;
+                    float* dst = reinterpret_cast<float*>(fp.accum + (size_t)sy*fp.w + sx);
+                    unsafeAtomicAdd(dst + 0, f*r.x);
+                    unsafeAtomicAdd(dst + 1, f*r.y);
+                    unsafeAtomicAdd(dst + 2, f*r.z);
+                    unsafeAtomicAdd(dst + 3, f);
+                }
+            }
+        } else {
+            float* dst = reinterpret_cast<float*>(fp.accum + pixel);
+            unsafeAtomicAdd(dst + 0, r.x);
+            unsafeAtomicAdd(dst + 1, r.y);
+            unsafeAtomicAdd(dst + 2, r.z);
+            unsafeAtomicAdd(dst + 3, 1.0f);
+        }
+    }
+}
+
 // k_pixel_map — the coordinates of every pixel of the shard's tile list, in list
 // order (tiles descending, raster inside a tile: RT/raytracer.cpp:555, :409-410),
 // so k_generate maps a sample to its pixel with one coalesced load.  One block per tile.
@@ -1211,7 +1268,12 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     // past them skip the ray setup entirely (about 2/3 of the pool is busy at any time).
     __shared__ uint16_t freelist[BLOCK];
     const uint32_t own = blockIdx.x*blockDim.x + threadIdx.x;
-    const bool own_free = own < pool.n && pool.state[own] == S_FREE;
+    const uint8_t own_state = own < pool.n ? pool.state[own] : (uint8_t)S_TRACE;
+    if (own_state == S_DONE) {                   // the previous iteration finished this path: splat it
+        splat_sample(fp, pool, own);
+        pool.state[own] = S_FREE;                // a claim below may reuse the slot (ordered by the barrier)
+    }
+    const bool own_free = own_state != S_TRACE;
     uint32_t nfree;
     const uint32_t rank = block_rank<BLOCK>(own_free, agg, &nfree);
     if (own_free) freelist[rank] = (uint16_t)threadIdx.x;
@@ -1641,66 +1703,16 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         pool.sh_c[spos] = make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f);
     }
     if (done) pool.state[slot] = S_DONE;
+    // slots the next k_generate may claim (scanned by k_bookkeep): finished now or idle; and
+    // the finished ones it must splat first (the host's termination test waits for them)
+    const bool idle = slot < pool.n && !valid;
+    const bool unsplat = done || (idle && pool.state[slot] == S_DONE);
+    uint32_t nfree;
+    (void)block_rank<BLOCK>(done || idle, agg, &nfree);
+    if (threadIdx.x == 0) pool.free_n[blockIdx.x] = nfree;
+    block_count<BLOCK>(&cnt->unsplat[shard][0], unsplat, agg);
 }
 
-// k_splat — vignette + splat_filter (RT/raytracer.cpp:469-488, 187-259) with
-// float atomics, then the slot returns to the free list.
-__global__ void __launch_bounds__(BLOCK) k_splat(FrameParams fp, Pool pool, Counters* cnt) {
-    const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
-    const bool valid = slot < pool.n && pool.state[slot] == S_DONE;
-    if (valid) {
-        const float4 L = pool.L[slot];
-        const float vig = pool.thr[slot].w;
-        const float2 j = pool.jitter[slot];
-        V3 r = muls(ld3(L), vig);
-        const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
-        if (fp.list_xy) {
-            const uint32_t k = __float_as_uint(pool.ray_d[slot].w);
-            float* o = fp.list_out + 5*(size_t)k;
-            o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = j.x; o[4] = j.y;
-        } else if (fp.samp_rgbx) {
-            // deterministic path: store the sample; k_resolve gathers it in reference order
-            const size_t rec = (size_t)__float_as_uint(pool.ray_d[slot].w)*fp.pixels + __float_as_uint(pool.prev_n[slot].w);
-            fp.samp_rgbx[rec] = make_float4(r.x, r.y, r.z, j.x);
-            fp.samp_jy[rec] = j.y;
-        } else if (fp.cache_size) {
-            const int64_t x = pixel % fp.w, y = pixel / fp.w;
-            const int64_t ks = fp.kernel_size;
-            const float kscale = (float)(fp.cache_size - 1) / (float)ks;
-            int64_t x0 = x - ks, x1 = x + ks + 1, y0 = y - ks, y1 = y + ks + 1;
-            int64_t xm = 0, ym = 0;
-            if (x0 < 0) { xm = -x0; x0 = 0; }
-            if (y0 < 0) { ym = -y0; y0 = 0; }
-            if (x1 > (int64_t)fp.w) x1 = fp.w;
-            if (y1 > (int64_t)fp.h) y1 = fp.h;
-            for (int64_t sy = y0; sy < y1; ++sy) {
-                int32_t jy = (int32_t)fabsf(0.5f + kscale*((float)(ym + (sy - y0) - ks) - j.y));
-                float fy = fp.lut[jy];
-                for (int64_t sx = x0; sx < x1; ++sx) {
-                    int32_t jx = (int32_t)fabsf(0.5f + kscale*((float)(xm + (sx - x0) - ks) - j.x));
-                    float f = fp.lut[jx]*fy;
-                    float* dst = reinterpret_cast<float*>(fp.accum + (size_t)sy*fp.w + sx);
-                    unsafeAtomicAdd(dst + 0, f*r.x);
-                    unsafeAtomicAdd(dst + 1, f*r.y);
-                    unsafeAtomicAdd(dst + 2, f*r.z);
-                    unsafeAtomicAdd(dst + 3, f);
-                }
-            }
-        } else {
-            float* dst = reinterpret_cast<float*>(fp.accum + pixel);
-            unsafeAtomicAdd(dst + 0, r.x);
-            unsafeAtomicAdd(dst + 1, r.y);
-            unsafeAtomicAdd(dst + 2, r.z);
-            unsafeAtomicAdd(dst + 3, 1.0f);
-        }
-    }
-    if (valid) pool.state[slot] = S_FREE;
-    // free slots of this block for the next k_generate's claims (scanned by k_bookkeep)
-    __shared__ uint32_t agg[BLOCK / 64 + 1];
-    uint32_t nfree;
-    (void)block_rank<BLOCK>(slot < pool.n && (valid || pool.state[slot] == S_FREE), agg, &nfree);
-    if (threadIdx.x == 0) pool.free_n[blockIdx.x] = nfree;
-}
 
 // k_resolve — splat_filter as a gather (RT/raytracer.cpp:187-259, :476-488).
 // Every output pixel sums its neighbours' samples in exactly the order the
@@ -1828,11 +1840,13 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         if (!first) {
             const unsigned long long rem = remaining_samples(cnt);
             cnt->next_sample += ((unsigned long long)cnt->gen_free < rem ? (unsigned long long)cnt->gen_free : rem);
-            uint32_t ext = 0, sh = 0, pend = 0, tq = 0, ts = 0;
+            uint32_t ext = 0, sh = 0, pend = 0, tq = 0, ts = 0, ps = 0;
             for (int k = 0; k < NSHARD; ++k) {
                 ext += cnt->cast[0][k][0] + cnt->alive[k][0];
                 sh += cnt->cast[1][k][0];
                 pend += cnt->alive[k][0];
+                ps += cnt->unsplat[k][0];
+                cnt->unsplat[k][0] = 0;
                 tq += cnt->ext_count[cur][k][0];
                 ts += cnt->shadow_count[k][0];
                 cnt->cast[0][k][0] = 0;
@@ -1848,6 +1862,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             cnt->traced_rays[0] += tq;
             cnt->traced_rays[1] += ts;
             cnt->pending = pend;
+            cnt->pending_splat = ps;
         }
         carry = 0;
     }
@@ -2243,7 +2258,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     if ((unsigned long long)pool_n*nparts > total) nparts = 1;
     if ((unsigned long long)pool_n > total) pool_n = (uint32_t)std::max<unsigned long long>(total, 1ull);
     pool_n = (pool_n + BLOCK - 1) / BLOCK * BLOCK;
-    const uint32_t prof = g_profiling;
+    const uint32_t prof = g_profiling & ~(1u << RT_KERNEL_SPLAT);   // the splat runs inside k_generate
     const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(s->start_ev, stream));
@@ -2312,9 +2327,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
         if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
-        e(RT_KERNEL_CONNECT); b(RT_KERNEL_SPLAT);
-        k_splat<<<r.grid, BLOCK, 0, q>>>(fp, pt.pool, pt.cnt);
-        e(RT_KERNEL_SPLAT);
+        e(RT_KERNEL_CONNECT);
         k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pt.pool, r.grid, r.cur, 0);
         ++r.iters;
         r.cur ^= 1;
@@ -2352,7 +2365,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             harvest(k, b);
             ++r.consumed;
             const Counters& c = s->part[k].cnt_host[b];
-            if (c.next_sample >= c.total_samples && c.pending == 0) {
+            if (c.next_sample >= c.total_samples && c.pending == 0 && c.pending_splat == 0) {
                 r.live = false; r.final_buf = b; --live;       // its chunk still in flight finds nothing to do
             } else {
                 int err = enqueue_chunk(k);
