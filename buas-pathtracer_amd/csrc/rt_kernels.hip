@@ -92,6 +92,11 @@ struct DevScene {
     uint32_t blob_q;                // float4 count (<= LDS_SCENE_Q)
     uint32_t off[10];               // byte offsets of the tables in the blob (BLOB_*)
 };
+// The 16 KB strata table is read at bounce 0 only (a few lookups per path): copying
+// it into every block's LDS costs more than the L2 reads it saves
+#ifndef RT_LDS_STRATA
+#define RT_LDS_STRATA 0
+#endif
 enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_TOP_SEQ, BLOB_LEAF_REC,
        BLOB_MESHES, BLOB_STRATA, BLOB_COUNT };
 constexpr uint32_t LDS_SCENE_Q = 2048;   // 32 KB
@@ -114,7 +119,9 @@ RT_D DevScene scene_in_lds(const DevScene& sc, float4* lds) {
     if (sc.top_seq) s.top_seq = reinterpret_cast<const float4*>(b + sc.off[BLOB_TOP_SEQ]);
     s.leaf_rec = reinterpret_cast<const float4*>(b + sc.off[BLOB_LEAF_REC]);
     s.meshes = reinterpret_cast<const DevMesh*>(b + sc.off[BLOB_MESHES]);
+#if RT_LDS_STRATA
     s.strata = reinterpret_cast<const uint8_t*>(b + sc.off[BLOB_STRATA]);
+#endif
     return s;
 }
 
@@ -1187,7 +1194,10 @@ RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return b
 // ======================================================================
 // Kernels
 // ======================================================================
-constexpr int BLOCK = 512;          // slot-ordered kernels (generate / shade / splat)
+#ifndef RT_BLOCK
+#define RT_BLOCK 256
+#endif
+constexpr int BLOCK = RT_BLOCK;      // slot-ordered kernels (generate / shade)
 constexpr int EV_SLOTS = 8;     // iterations in flight per partition in run_frame (2 chunks of 4)
 
 // The splat of a finished path (RT/raytracer.cpp:469-488): vignette, then the
@@ -2685,7 +2695,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         put(BLOB_TOP_SEQ, top_seq_host.data(), top_seq_host.size()*sizeof(float4));
         put(BLOB_LEAF_REC, leaf_rec_host.data(), (size_t)d->bvh_index_count*LEAF_REC_Q*sizeof(float4));
         put(BLOB_MESHES, meshes.data(), meshes.size()*sizeof(DevMesh));
+#if RT_LDS_STRATA
         put(BLOB_STRATA, rt_dev_strata_tab, sizeof(rt_dev_strata_tab));
+#else
+        put(BLOB_STRATA, nullptr, 0);
+#endif
         const char* env = getenv("RT_LDS_SCENE");               // 0: the kernels read the tables from HBM
         ds.blob = nullptr; ds.blob_q = 0;
         if (blob.size() <= 16*(size_t)LDS_SCENE_Q && !(env && env[0] == '0')) {

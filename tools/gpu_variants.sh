@@ -5,6 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/variants
 ARGS=${BENCH_ARGS:-"--spp 64 --steps 2 --warmup 1 --no-cpu-baseline"}
 for lib in buas-pathtracer_amd/lib/librt_mi355x.so buas-pathtracer_amd/lib/variants/*/librt_mi355x.so; do
+  [ -f "$lib" ] || continue
   name=$(basename $(dirname $lib)); [ "$name" = lib ] && name=default
   RT_MI355X_LIB=$PWD/$lib timeout -k 10 ${BENCH_TIMEOUT:-300} python bench.py $ARGS > gpurun_out/variants/$name.log 2>&1
   rc=$?
