@@ -100,6 +100,9 @@ struct DevScene {
 enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_TOP_SEQ, BLOB_LEAF_REC,
        BLOB_MESHES, BLOB_STRATA, BLOB_COUNT };
 constexpr uint32_t LDS_SCENE_Q = 2048;   // 32 KB
+// The copy is the launch's dynamic LDS, sized to the blob (blob_q float4): a fixed
+// 32 KB array held 256-thread blocks to 5 per CU whatever the scene's size.
+extern __shared__ float4 lds_scene[];
 
 // The scene seen through the LDS copy: every small table's pointer rebased onto
 // `lds` (generic pointers, so the code that reads them is unchanged).  All
@@ -1270,7 +1273,6 @@ __global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out
 __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                     Counters* cnt, int cur) {
     __shared__ uint32_t agg[BLOCK / 64 + 1];
-    __shared__ float4 lds_scene[LDS_SCENE_Q];
     const DevScene sc = scene_in_lds(sc_g, lds_scene);
     // Free slots claim consecutive sample numbers in slot order: the block's first
     // claim is the scan of the free counts k_bookkeep made (no atomics).  The block's
@@ -1376,7 +1378,10 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
 // Persistent waves: each wave grabs CHUNK queue items with one atomic and
 // refills lanes whose query has finished from that chunk (Aila & Laine 2009,
 // for 64-wide waves), so lanes do not idle behind the wave's longest ray.
-constexpr int TB = 256;
+#ifndef RT_TB
+#define RT_TB 256
+#endif
+constexpr int TB = RT_TB;
 constexpr uint32_t CHUNK = 256;
 #ifndef RT_STEPS_PER_REFILL
 #define RT_STEPS_PER_REFILL 8
@@ -1398,6 +1403,11 @@ constexpr int STEPS_PER_REFILL_SHADOW = RT_STEPS_PER_REFILL_SHADOW;
 // the kernel is built without the top-level walk.
 template <bool OCC, bool LST>
 __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag) {
+#ifdef RT_TRACE_PRIO
+    // trace waves are latency bound and issue little; shade waves sharing the SIMD are
+    // issue bound: let a trace wave's next load go out first
+    __builtin_amdgcn_s_setprio(RT_TRACE_PRIO);
+#endif
     __shared__ uint2 lds_stack[STACK_LDS*TB];
     Stack st;
     st.lds = lds_stack; st.spill = spill; st.lane = threadIdx.x; st.block = TB;
@@ -1506,7 +1516,6 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur) {
     __shared__ uint32_t agg[BLOCK / 64 + 1];
-    __shared__ float4 lds_scene[LDS_SCENE_Q];
     const DevScene sc = scene_in_lds(sc_g, lds_scene);
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const bool valid = slot < pool.n && pool.state[slot] == S_TRACE;   // traced this iteration
@@ -2328,12 +2337,12 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         auto b = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
         auto e = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
         b(RT_KERNEL_GENERATE);
-        k_generate<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        k_generate<<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
         if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
-        k_shade<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        k_shade<<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
         if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
