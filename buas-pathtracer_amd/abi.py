@@ -173,6 +173,7 @@ ABI_FUNCTIONS = {
                                      P(C.c_uint32)]),
     "rt_debug_top_sequences": (C.c_int, [P(BvhNode), C.c_uint32, C.c_uint32, P(C.c_float), C.c_uint32,
                                          P(C.c_uint32)]),
+    "rt_debug_verify_rcp": (C.c_int, [C.c_int, P(C.c_uint64), P(C.c_uint32)]),
     "rt_set_profiling": (C.c_int, [C.c_int]),
     "rt_set_profiling_stages": (C.c_int, [C.c_uint32]),
     "rt_set_path_pool": (C.c_int, [C.c_uint32]),

@@ -35,6 +35,27 @@ RT_D V3 smul(float s, V3 a) { return {s * a.x, s * a.y, s * a.z}; }
 RT_D V3 divs(V3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
 RT_D V3 sdiv(float s, V3 a) { return {s / a.x, s / a.y, s / a.z}; }
 RT_D V3 neg(V3 a) { return {-a.x, -a.y, -a.z}; }
+// 1.0f / x, correctly rounded, in 3 VALU instead of the 11-instruction division
+// expansion (div_scale x2, rcp, 5 fma, mul, div_fmas, div_fixup): v_rcp_f32's estimate
+// refined by one Newton step on the FMA residual, for |x| in [2^-125, 2^125], where
+// neither the residual nor the result leaves the normal range.  Other inputs (zeros,
+// denormals, huge values, inf, NaN) take the full division; a wave whose lanes are all
+// in range skips it.  rt_debug_verify_rcp checks it against the IEEE division for
+// every one of the 2^32 floats (tests/test_gpu_parity.py::test_rcp_cr_exhaustive).
+#ifndef RT_RCP_CR
+#define RT_RCP_CR 1
+#endif
+RT_D float rcp_cr(float x) {
+#if RT_RCP_CR
+    const float a = __builtin_fabsf(x);
+    if (a >= 0x1p-125f && a <= 0x1p125f) {
+        const float r = __builtin_amdgcn_rcpf(x);
+        return __builtin_fmaf(__builtin_fmaf(-x, r, 1.0f), r, r);
+    }
+#endif
+    return 1.0f / x;
+}
+RT_D V3 rcp3(V3 a) { return {rcp_cr(a.x), rcp_cr(a.y), rcp_cr(a.z)}; }
 RT_D float dot(V3 a, V3 b) { return a.x*b.x + a.y*b.y + a.z*b.z; }
 RT_D V3 cross(V3 a, V3 b) { return {a.y*b.z - a.z*b.y, a.z*b.x - a.x*b.z, a.x*b.y - a.y*b.x}; }
 RT_D float length_sq(V3 a) { return dot(a, a); }
@@ -43,7 +64,7 @@ RT_D float mx(float a, float b) { return a > b ? a : b; }
 RT_D float clampf_(float n, float a, float b) { return mx(a, mn(b, n)); }
 RT_D float max3(V3 a) { return mx(a.x, mx(a.y, a.z)); }
 RT_D V3 vabs(V3 a) { return {fabsf(a.x), fabsf(a.y), fabsf(a.z)}; }
-RT_D V3 normalize(V3 a) { float r = 1.0f / __builtin_sqrtf(dot(a, a)); return muls(a, r); }
+RT_D V3 normalize(V3 a) { float r = rcp_cr(__builtin_sqrtf(dot(a, a))); return muls(a, r); }
 RT_D V3 noz(V3 a) {
     V3 r = {0.0f, 0.0f, 0.0f};
     float lsq = length_sq(a);
@@ -162,7 +183,7 @@ RT_D float d_atanf(float xx) {
     int sgn = 0;
     if (x < 0.0f) { sgn = 1; x = -x; }
     float y;
-    if (x > 2.414213562373095f) { y = 1.5707963267948966192f; x = -(1.0f / x); }
+    if (x > 2.414213562373095f) { y = 1.5707963267948966192f; x = -rcp_cr(x); }
     else if (x > 0.4142135623730950f) { y = 0.7853981633974483096f; x = (x - 1.0f) / (x + 1.0f); }
     else { y = 0.0f; }
     float z = x * x;

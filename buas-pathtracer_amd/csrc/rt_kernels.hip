@@ -133,7 +133,7 @@ struct Ray { V3 o, d, inv_d; uint32_t neg; float max_t; uint32_t zero; };   // z
 RT_D Ray make_ray(V3 o, V3 d, float far_clip) {              // RT/intersection.h:13-24
     Ray r;
     r.o = o; r.d = d;
-    r.inv_d = sdiv(1.0f, d);
+    r.inv_d = rcp3(d);
     r.neg = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
     r.zero = (d.x == 0.0f ? 1u : 0u) | (d.y == 0.0f ? 2u : 0u) | (d.z == 0.0f ? 4u : 0u);
     r.max_t = far_clip;
@@ -238,7 +238,7 @@ RT_D bool ray_triangle(const Ray& ray, V3 a, V3 e1, V3 e2, float& t, float& ov, 
     V3 pvec = cross(ray.d, e2);
     float det = dot(e1, pvec);
     if (det > -eps && det < eps) return false;
-    float inv_det = 1.0f / det;
+    float inv_det = rcp_cr(det);
     V3 tvec = sub(ray.o, a);
     float v = dot(tvec, pvec)*inv_det;
     if (v < 0.0f || v > 1.0f) return false;
@@ -302,6 +302,34 @@ RT_D void unpack_node(const rt_bvh_node* nodes, uint32_t x, uint32_t& lf, uint32
 //   sphere/box: q3.zw = p[0], p[1]; q4.x = p[2]
 //   mesh:       q3.zw = node_off, tri_off; q4 = root record, root bv_p.xyz; q5 = root bv_r.xyz
 constexpr int LEAF_REC_Q = 6;
+// q3.y: the primitive type in bits 0-7; LEAF_TRANSLATE: the inverse's 3x3 part is
+// exactly the identity and its translation finite (spheres and unrotated boxes)
+constexpr uint32_t LEAF_TRANSLATE = 0x100u;
+
+// transform_ray (RT/intersection.cpp:403-409) into a leaf record's object space.  For a
+// translation-only inverse the 3x4 products reduce to adding the translation, bit for
+// bit, when every component of o and d is finite and non-zero (`plain`): x*1 = x,
+// y*0 = +-0 and x + (+-0) = x for x != 0, and 0*t = +-0 for a finite t.  A wave with a
+// lane that is not plain takes the full product for that lane.
+RT_D bool plain_ray(V3 o, V3 d) {
+    const V3 ao = vabs(o), ad = vabs(d);
+    const float m = fminf(fminf(fminf(ao.x, ao.y), fminf(ao.z, ad.x)), fminf(ad.y, ad.z));
+    const float sum = ((ao.x + ao.y) + (ao.z + ad.x)) + (ad.y + ad.z);   // NaN or inf (or overflow): not plain
+    return m > 0.0f && sum < __builtin_inff();
+}
+RT_D void object_ray(float4 q0, float4 q1, float4 q2, bool translate, bool plain, V3 o, V3 d, V3& io, V3& id) {
+    if (translate && plain) {
+        io = {o.x + q0.w, o.y + q1.w, o.z + q2.w};
+        id = d;
+    } else {
+        M34 inv;
+        inv.e[0][0] = q0.x; inv.e[0][1] = q0.y; inv.e[0][2] = q0.z; inv.e[0][3] = q0.w;
+        inv.e[1][0] = q1.x; inv.e[1][1] = q1.y; inv.e[1][2] = q1.z; inv.e[1][3] = q1.w;
+        inv.e[2][0] = q2.x; inv.e[2][1] = q2.y; inv.e[2][2] = q2.z; inv.e[2][3] = q2.w;
+        io = xform(inv, o, 1.0f);
+        id = xform(inv, d, 0.0f);
+    }
+}
 
 // ----------------------------------------------------------------------
 // Scene traversal as a step machine.
@@ -443,6 +471,7 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
     uint32_t list = 0, n = 0, next = 0;
     bool full = false;
     const uint32_t len = sc.top_seq_len;
+    const bool plain = plain_ray(o, d);
     for (uint32_t i = 0; i < len; ++i) {
         const float4 a = ld_uniform(seq + 2*i), b = ld_uniform(seq + 2*i + 1);
         const uint32_t info = __float_as_uint(b.z), skip = __float_as_uint(b.w);
@@ -457,27 +486,29 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
         for (uint32_t j = first; j < end; ++j) {                   // the leaf's primitives in order
             const float4* q = sc.leaf_rec + (size_t)j*LEAF_REC_Q;
             const float4 q3 = ld_uniform(q + 3);
-            const uint32_t pi = __float_as_uint(q3.x), type = __float_as_uint(q3.y);
+            const uint32_t pi = __float_as_uint(q3.x), tword = __float_as_uint(q3.y), type = tword & 0xFFu;
             if (!pass || pi == ignored) continue;
-            M34 inv;
             const float4 q0 = ld_uniform(q), q1 = ld_uniform(q + 1), q2 = ld_uniform(q + 2);
-            inv.e[0][0] = q0.x; inv.e[0][1] = q0.y; inv.e[0][2] = q0.z; inv.e[0][3] = q0.w;
-            inv.e[1][0] = q1.x; inv.e[1][1] = q1.y; inv.e[1][2] = q1.z; inv.e[1][3] = q1.w;
-            inv.e[2][0] = q2.x; inv.e[2][1] = q2.y; inv.e[2][2] = q2.z; inv.e[2][3] = q2.w;
-            const Ray ir = make_ray(xform(inv, o, 1.0f), xform(inv, d, 0.0f), 0.0f);   // transform_ray :403-409
-            if (type == RT_PRIMITIVE_MESH) {                       // the mesh root's pop-time test (:269-275)
-                const float4 q4 = ld_uniform(q + 4), q5 = ld_uniform(q + 5);
-                float tm;
-                if (bv_static(ir, {q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z}, tm) && tm < r.t) {
-                    if (n < sc.mlist_max) list |= j << (6*n);
-                    else full = true;
-                    ++n;
-                }
-                continue;
-            }
+            V3 io, id;
+            object_ray(q0, q1, q2, tword & LEAF_TRANSLATE, plain, o, d, io, id);   // transform_ray :403-409
             bool hit = false;
-            if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, q3.z, r.t);
-            else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {q3.z, q3.w, ld_uniform(q + 4).x}, r.t);
+            if (type == RT_PRIMITIVE_SPHERE) {                     // needs no 1/d
+                Ray ir; ir.o = io; ir.d = id;
+                hit = ray_sphere(ir, q3.z, r.t);
+            } else {
+                const Ray ir = make_ray(io, id, 0.0f);
+                if (type == RT_PRIMITIVE_MESH) {                   // the mesh root's pop-time test (:269-275)
+                    const float4 q4 = ld_uniform(q + 4), q5 = ld_uniform(q + 5);
+                    float tm;
+                    if (bv_static(ir, {q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z}, tm) && tm < r.t) {
+                        if (n < sc.mlist_max) list |= j << (6*n);
+                        else full = true;
+                        ++n;
+                    }
+                    continue;
+                }
+                if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {q3.z, q3.w, ld_uniform(q + 4).x}, r.t);
+            }
             if (hit) {
                 r.code = pi;
                 if (occ) { r.occluded = true; pass = false; next = 0xFFFFFFFFu; }
@@ -499,7 +530,7 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
         for (uint32_t j = first; j < end; ++j) {                   // the leaf's primitives in order
             const float4* q = sc.leaf_rec + (size_t)j*LEAF_REC_Q;
             const float4 q3 = q[3];
-            const uint32_t pi = __float_as_uint(q3.x), type = __float_as_uint(q3.y);
+            const uint32_t pi = __float_as_uint(q3.x), type = __float_as_uint(q3.y) & 0xFFu;
             if (pi == ignored) continue;
             M34 inv;
             const float4 q0 = q[0], q1 = q[1], q2 = q[2];
@@ -731,7 +762,7 @@ struct Traversal {
             const uint32_t pi = __float_as_uint(F[3].x);
             ++leaf_cur; leaf_list >>= 6;
             if (pi == ignored) return true;
-            const uint32_t type = __float_as_uint(F[3].y);
+            const uint32_t type = __float_as_uint(F[3].y) & 0xFFu;
             M34 inv;
             inv.e[0][0] = F[0].x; inv.e[0][1] = F[0].y; inv.e[0][2] = F[0].z; inv.e[0][3] = F[0].w;
             inv.e[1][0] = F[1].x; inv.e[1][1] = F[1].y; inv.e[1][2] = F[1].z; inv.e[1][3] = F[1].w;
@@ -907,7 +938,7 @@ RT_D V3 random_in_unit_sphere(Rng& e) {                                   // :11
 }
 RT_D V3 oriented_around_normal(V3 v, V3 n) {                             // :58-75
     float sign = copy_sign(1.0f, n.z);
-    float a = -1.0f / (sign + n.z);
+    float a = -rcp_cr(sign + n.z);                 // -1/x == -(1/x) exactly
     float b = n.x*n.y*a;
     V3 T = {1.0f + sign*n.x*n.x*a, sign*b, -sign*n.x};
     V3 B = {b, sign + n.y*n.y*a, -n.y};
@@ -991,7 +1022,7 @@ RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float
         out_p = pdf / sum;
         return sc.lights[li];
     }
-    out_p = 1.0f / (float)n;
+    out_p = rcp_cr((float)n);
     float f = rs*(float)n - EPSILON;
     uint32_t li = f <= 0.0f ? 0u : (uint32_t)f;
     if (li >= n) li = n - 1;
@@ -1147,6 +1178,50 @@ RT_D void block_count(uint32_t* counter, bool pred, uint32_t* scratch) {
     uint32_t total;
     (void)block_rank<NT>(pred, scratch, &total);
     if (threadIdx.x == 0 && total) atomicAdd(counter, total);
+}
+
+// K block-wide tallies at once (the end of k_generate / k_shade): one ballot per
+// predicate, ONE barrier to publish the per-wave counts, then thread 0 scans the
+// waves and adds each tally's block total to ctr[k] (a null ctr: total only), all K
+// atomics in flight together; one barrier to publish the bases.  The
+// separate block_count / block_append calls this replaces cost 3 barriers and a
+// serialized atomic round trip each (13 % of a k_shade wave's time).
+// pos[k] = the counter's old value + the thread's rank among the block's threads
+// with pred[k] (an append position); total[k] = the block's count.
+// scratch: LDS of (NT/64 + 2)*K words, not reused by the caller afterwards.
+template <int NT, int K>
+RT_D void block_tally(const bool (&pred)[K], uint32_t* const (&ctr)[K], uint32_t (&pos)[K], uint32_t (&total)[K],
+                      uint32_t* scratch) {
+    constexpr int NW = NT / 64;
+    const uint32_t lane = __lane_id();
+    const uint32_t wave = threadIdx.x / 64;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    unsigned long long mask[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        mask[k] = __ballot(pred[k]);
+        if (lane == 0) scratch[wave*K + k] = (uint32_t)__popcll(mask[k]);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {                 // static indices only: no pointer table in scratch
+        uint32_t t[K], base[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            t[k] = 0;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) { const uint32_t c = scratch[w*K + k]; scratch[w*K + k] = t[k]; t[k] += c; }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) base[k] = (ctr[k] && t[k]) ? atomicAdd(ctr[k], t[k]) : 0u;   // K in flight
+#pragma unroll
+        for (int k = 0; k < K; ++k) { scratch[NW*K + k] = base[k]; scratch[(NW + 1)*K + k] = t[k]; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        pos[k] = scratch[NW*K + k] + scratch[wave*K + k] + (uint32_t)__popcll(mask[k] & lt);
+        total[k] = scratch[(NW + 1)*K + k];
+    }
 }
 
 RT_D unsigned long long remaining_samples(const Counters* c) { return c->total_samples - c->next_sample; }
@@ -1361,8 +1436,12 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     }
     // new paths that enter the BVH go to the current extension queue behind the survivors
     const uint32_t shard = blockIdx.x % NSHARD;
-    block_count<BLOCK>(&cnt->cast[0][shard][0], cast, agg);
-    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[cur][shard][0], enqueue, agg);
+    __shared__ uint32_t tally[(BLOCK / 64 + 2)*2];
+    const bool tp[2] = {enqueue, cast};
+    uint32_t* const tc[2] = {&cnt->ext_count[cur][shard][0], &cnt->cast[0][shard][0]};
+    uint32_t tpos[2], ttot[2];
+    block_tally<BLOCK, 2>(tp, tc, tpos, ttot, tally);
+    const uint32_t pos = tpos[0];
     if (enqueue) {
         float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + pos);
         q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
@@ -1513,12 +1592,29 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 #else
 #define RT_SHADE_ATTR
 #endif
+#if RT_SHADE_PROF
+// Measurement build only (-DRT_SHADE_PROF=1): wave time per k_shade section, s_memtime
+// cycles summed over waves (the max over a wave's lanes: a divergent section costs the
+// wave whether one lane or all take it); printed to stderr after every frame.
+enum { SP_LOAD, SP_GEOM, SP_EMIS, SP_FRES, SP_REFL, SP_REFR, SP_NEE, SP_IND, SP_RR, SP_SKY, SP_SHPRO, SP_CPRO,
+       SP_STORE, SP_TAIL, SP_TOTAL, SP_N };
+__device__ unsigned long long g_shade_prof[SP_N + 1];
+#define SP_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define SP_ADD(i, a) prof[i] += __builtin_amdgcn_s_memtime() - (a)
+#else
+#define SP_MARK(v)
+#define SP_ADD(i, a)
+#endif
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur) {
-    __shared__ uint32_t agg[BLOCK / 64 + 1];
+#if RT_SHADE_PROF
+    unsigned long long prof[SP_N] = {};
+    SP_MARK(t_start);
+#endif
     const DevScene sc = scene_in_lds(sc_g, lds_scene);
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
-    const bool valid = slot < pool.n && pool.state[slot] == S_TRACE;   // traced this iteration
+    const uint8_t state0 = slot < pool.n ? pool.state[slot] : (uint8_t)S_FREE;
+    const bool valid = slot < pool.n && state0 == S_TRACE;             // traced this iteration
     bool cont = false, done = false, shadow = false, cast_shadow = false, enq = false;
     Prologue spro = {}, cpro = {};
     V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
@@ -1526,6 +1622,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     float sh_t = 0.0f;
     uint32_t sh_light = 0;
     if (valid) {
+        SP_MARK(t_load);
         const float4 o4 = pool.ray_o[slot], d4 = pool.ray_d[slot];
         const float4 t4 = pool.thr[slot], L4 = pool.L[slot], pn4 = pool.prev_n[slot];
         const float4 h4 = pool.hit[slot];
@@ -1544,7 +1641,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         Hit h;
         h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = pool.hit_w[slot];
         Ray ray; ray.o = ro; ray.d = rd;
+        SP_ADD(SP_LOAD, t_load);
         if (h.code != RT_HIT_MISS) {
+            SP_MARK(t_geom);
             V3 I, N;
             uint32_t surf_id;
             hit_geometry(sc, ray, h, I, N, surf_id);
@@ -1563,11 +1662,13 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             }
             const rt_material mi = sc.materials[mi_id];
             const rt_material mt = sc.materials[mt_id];
+            SP_ADD(SP_GEOM, t_geom);
             if (mi.is_participating_medium) {                                  // Beer :640-649
                 V3 ab = {d_expf(-mi.absorb.x*t), d_expf(-mi.absorb.y*t), d_expf(-mi.absorb.z*t)};
                 thr = mul(thr, ab);
             }
             if (mt.flags & RT_MATERIAL_EMISSIVE) {                             // :651-670
+                SP_MARK(t_emis);
                 bool allow = (!st.next_event_estimation ||
                               ((st.caustics || (bounce < 2)) && is_spec));
                 if (allow) {
@@ -1577,10 +1678,12 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                     float light_pdf = ldsq / cos_i;
                     float brdf_pdf = (st.importance_sample_diffuse ? dot(prev_N, rd) / PI_32 : 1.0f / (2.0f*PI_32));
                     float mis_pdf = light_pdf + brdf_pdf;
-                    total = add(total, mul(smul(1.0f / mis_pdf, thr), rv3(mt.emission_color)));
+                    total = add(total, mul(smul(rcp_cr(mis_pdf), thr), rv3(mt.emission_color)));
                 }
                 done = true;
+                SP_ADD(SP_EMIS, t_emis);
             } else {
+                SP_MARK(t_fres);
                 float eta_i = mi.ior, eta_t = mt.ior;
                 float eta = eta_i / eta_t;
                 float cos_t;
@@ -1588,7 +1691,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                 float reflect_test = sample_1d(sc, ss, rng, S_Reflectance, bounce);
                 refl = lerpf_(refl, 1.0f, mt.metallic);
                 is_spec = 1;
+                SP_ADD(SP_FRES, t_fres);
                 if (reflect_test < refl) {                                      // reflect :684-696
+                    SP_MARK(t_refl);
                     V3 nd = reflect(rd, N);
                     if (mt.roughness > 0.0f) {
                         V3 rs = random_in_unit_sphere(rng);
@@ -1596,7 +1701,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                     }
                     ro = add(I, smul(EPSILON, nd)); rd = nd;
                     thr = mul(thr, lerp3(v3s(1.0f), rv3(mt.albedo), mt.metallic));
+                    SP_ADD(SP_REFL, t_refl);
                 } else if (mt.is_participating_medium) {                       // refract :698-717
+                    SP_MARK(t_refr);
                     if (inside) {
                         if (at > 0) --at;
                     } else if (at < 63) {
@@ -1605,7 +1712,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                     }
                     V3 fd = add(smul(eta, rd), muls(N, (eta*cos_i - cos_t)));
                     ro = add(I, muls(fd, EPSILON)); rd = fd;
+                    SP_ADD(SP_REFR, t_refr);
                 } else {                                                        // diffuse :718-790
+                    SP_MARK(t_nee);
                     is_spec = 0;
                     V3 albedo = evaluate_material(mt, I);
                     V3 brdf = smul(1.0f / PI_32, albedo);
@@ -1633,11 +1742,11 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                                 float sa = (nndl * A) / dsq;
                                 float pdf;
                                 if (st.use_mis) {
-                                    float lpdf = 1.0f / sa;
+                                    float lpdf = rcp_cr(sa);
                                     float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
                                     pdf = lpdf + bpdf;
                                 } else {
-                                    pdf = 1.0f / sa;
+                                    pdf = rcp_cr(sa);
                                 }
                                 pdf *= lrp;
                                 sh_c = mul(mul(muls(thr, dot(N, Lv) / pdf), brdf),
@@ -1650,6 +1759,8 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                             }
                         }
                     }
+                    SP_ADD(SP_NEE, t_nee);
+                    SP_MARK(t_ind);
                     V2 s2 = sample_2d(sc, ss, rng, S_IndirectLighting, bounce); // indirect :777-789
                     V3 R;
                     if (st.importance_sample_diffuse) {
@@ -1661,12 +1772,15 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                     }
                     thr = mul(thr, brdf);
                     ro = add(I, muls(N, EPSILON)); rd = R;
+                    SP_ADD(SP_IND, t_ind);
                 }
                 if (st.russian_roulette && !is_spec) {                          // RR :801-811
+                    SP_MARK(t_rr);
                     float p = clampf_(max3(thr), 0.1f, 0.9f);
                     float e = sample_1d(sc, ss, rng, S_Roulette, bounce);
                     if (e > p) done = true;
-                    else thr = muls(thr, 1.0f / p);
+                    else thr = muls(thr, rcp_cr(p));
+                    SP_ADD(SP_RR, t_rr);
                 }
             }
             if (!done) {
@@ -1675,44 +1789,61 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                 if (bounce >= st.max_bounce_count) done = true;
             }
         } else {
+            SP_MARK(t_sky);
             total = add(total, mul(thr, sample_sky(sc, rd)));                 // miss :812-815
             done = true;
+            SP_ADD(SP_SKY, t_sky);
         }
         if (cast_shadow) {
             // intersect_shadow_ray (:756): planes and the top level here; only rays that meet
             // a mesh are queued for k_trace<true>.  Nothing else adds to total_color after the
             // NEE term in a bounce, so adding it here keeps the reference's order (:768).
+            SP_MARK(t_shpro);
             spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
             shadow = !spro.occluded && spro.bvh;
             if (!spro.occluded && !spro.bvh) total = add(total, sh_c);
+            SP_ADD(SP_SHPRO, t_shpro);
         }
         cont = !done;
         nro = ro; nrd = rd;
         if (cont) {                                        // next bounce's intersect_scene: planes + top level here
+            SP_MARK(t_cpro);
             cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
             pool.hit[slot] = make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f);
             pool.hit_w[slot] = 0.0f;
             enq = cpro.bvh;
+            SP_ADD(SP_CPRO, t_cpro);
         }
+        SP_MARK(t_store);
         pool.ray_o[slot] = make_float4(ro.x, ro.y, ro.z, o4.w);
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, d4.w);
         pool.thr[slot] = make_float4(thr.x, thr.y, thr.z, t4.w);
         pool.L[slot] = make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at)));
         pool.prev_n[slot] = make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
+        SP_ADD(SP_STORE, t_store);
     }
+    SP_MARK(t_tail);
     const int nxt = cur ^ 1;
     const uint32_t shard = blockIdx.x % NSHARD;
-    block_count<BLOCK>(&cnt->alive[shard][0], cont, agg);
-    block_count<BLOCK>(&cnt->cast[1][shard][0], cast_shadow, agg);
-    uint32_t pos = block_append<BLOCK>(&cnt->ext_count[nxt][shard][0], enq, agg);
+    // slots the next k_generate may claim (scanned by k_bookkeep): finished now or idle; and
+    // the finished ones it must splat first (the host's termination test waits for them)
+    const bool idle = slot < pool.n && !valid;
+    const bool unsplat = done || (idle && state0 == S_DONE);
+    __shared__ uint32_t tally[(BLOCK / 64 + 2)*6];
+    const bool tp[6] = {enq, shadow, cont, cast_shadow, unsplat, done || idle};
+    uint32_t* const tc[6] = {&cnt->ext_count[nxt][shard][0], &cnt->shadow_count[shard][0], &cnt->alive[shard][0],
+                             &cnt->cast[1][shard][0], &cnt->unsplat[shard][0], nullptr};
+    uint32_t tpos[6], ttot[6];
+    block_tally<BLOCK, 6>(tp, tc, tpos, ttot, tally);
+    const uint32_t pos = tpos[0];
     if (enq) {
         float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + pos);
         q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
         q[1] = make_float4(nrd.x, nrd.y, nrd.z, cpro.t);
         q[2] = make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, __uint_as_float(cpro.mlist));
     }
-    uint32_t spos = shard*pool.shard_cap + block_append<BLOCK>(&cnt->shadow_count[shard][0], shadow, agg);
+    const uint32_t spos = shard*pool.shard_cap + tpos[1];
     if (shadow) {
         pool.sh_slot[spos] = slot;
         float4* q = pool.sh_rec + REC_Q*(size_t)spos;
@@ -1722,14 +1853,18 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         pool.sh_c[spos] = make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f);
     }
     if (done) pool.state[slot] = S_DONE;
-    // slots the next k_generate may claim (scanned by k_bookkeep): finished now or idle; and
-    // the finished ones it must splat first (the host's termination test waits for them)
-    const bool idle = slot < pool.n && !valid;
-    const bool unsplat = done || (idle && pool.state[slot] == S_DONE);
-    uint32_t nfree;
-    (void)block_rank<BLOCK>(done || idle, agg, &nfree);
-    if (threadIdx.x == 0) pool.free_n[blockIdx.x] = nfree;
-    block_count<BLOCK>(&cnt->unsplat[shard][0], unsplat, agg);
+    if (threadIdx.x == 0) pool.free_n[blockIdx.x] = ttot[5];
+#if RT_SHADE_PROF
+    SP_ADD(SP_TAIL, t_tail);
+    SP_ADD(SP_TOTAL, t_start);
+    if (blockIdx.x % 128 == 0)      // a sample of the waves: the atomics must not load the memory system
+    for (int i = 0; i < SP_N; ++i) {
+        unsigned long long v = prof[i];
+        for (int m = 32; m; m >>= 1) { const unsigned long long u = __shfl_xor(v, m); v = u > v ? u : v; }
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_shade_prof[i], v);
+    }
+    if (blockIdx.x % 128 == 0 && (threadIdx.x & 63) == 0) atomicAdd(&g_shade_prof[SP_N], 1ull);
+#endif
 }
 
 
@@ -1968,6 +2103,20 @@ RT_D float remap_tpdf(float x) {                                                
     x = x - sign_of(x);
     return x;
 }
+// rt_debug_verify_rcp: rcp_cr against the IEEE division, 16 inputs per thread.
+__global__ void __launch_bounds__(256) k_verify_rcp(uint32_t base, unsigned long long* out) {
+    const uint32_t t = blockIdx.x*256 + threadIdx.x, stride = gridDim.x*256;
+    for (uint32_t i = 0; i < 16; ++i) {
+        const uint32_t bits = base + t + i*stride;
+        const float x = __uint_as_float(bits);
+        const float a = rcp_cr(x), b = 1.0f / x;
+        if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) {
+            atomicAdd(out, 1ull);
+            atomicMin(out + 1, (unsigned long long)bits);
+        }
+    }
+}
+
 __global__ void __launch_bounds__(256) k_post(const float4* px, uint32_t w, uint32_t h, rt_post_settings post,
                                               const uint8_t* noise, uint32_t* out) {
     const uint32_t x = blockIdx.x*64 + (threadIdx.x & 63), y = blockIdx.y*4 + (threadIdx.x >> 6);
@@ -2650,7 +2799,10 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 q[4] = make_float4(u2f(root), rn.bv_p.x, rn.bv_p.y, rn.bv_p.z);
                 q[5] = make_float4(rn.bv_r.x, rn.bv_r.y, rn.bv_r.z, 0.0f);
             } else {
-                q[3] = make_float4(u2f(pi), u2f(p.type), p.p[0], p.p[1]);
+                bool translate = std::isfinite(iv.e[0][3]) && std::isfinite(iv.e[1][3]) && std::isfinite(iv.e[2][3]);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) translate = translate && iv.e[r][c] == (r == c ? 1.0f : 0.0f);
+                q[3] = make_float4(u2f(pi), u2f(p.type | (translate ? LEAF_TRANSLATE : 0u)), p.p[0], p.p[1]);
                 q[4] = make_float4(p.p[2], 0.0f, 0.0f, 0.0f);
             }
         }
@@ -2907,6 +3059,18 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     HIP_OK(hipGetLastError());
     if (prof_resolve) HIP_OK(hipEventRecord(e1, stream));
     HIP_OK(hipStreamSynchronize(stream));
+#if RT_SHADE_PROF
+    {
+        static const char* names[SP_N] = {"load", "geom", "emis", "fres", "refl", "refr", "nee", "ind", "rr", "sky",
+                                          "shpro", "cpro", "store", "tail", "total"};
+        unsigned long long v[SP_N + 1] = {}, zero[SP_N + 1] = {};
+        HIP_OK(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_shade_prof), sizeof(v)));
+        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_shade_prof), zero, sizeof(zero)));
+        fprintf(stderr, "shade_prof waves=%llu", v[SP_N]);
+        for (int i = 0; i < SP_N; ++i) fprintf(stderr, " %s=%.1f", names[i], (double)v[i] / (double)(v[SP_N] ? v[SP_N] : 1));
+        fprintf(stderr, " (cycles per wave)\n");
+    }
+#endif
     if (stats) {
         stats->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (prof_resolve) {
@@ -2995,6 +3159,25 @@ int rt_debug_top_sequences(const rt_bvh_node* nodes, uint32_t node_count, uint32
     if (q.empty()) { set_error("top level too large for the prologue"); return RT_ERROR_INVALID; }
     if (out && out_cap_entries >= 8*len) memcpy(out, q.data(), q.size()*sizeof(float4));
     return (out && out_cap_entries < 8*len) ? RT_ERROR_INVALID : RT_OK;
+}
+
+int rt_debug_verify_rcp(int device, uint64_t* out_mismatches, uint32_t* out_first_bits) {
+    if (!out_mismatches || !out_first_bits) { set_error("null argument"); return RT_ERROR_INVALID; }
+    int err = bind_device(device);
+    if (err) return err;
+    unsigned long long* d = nullptr;
+    HIP_OK(hipMalloc(&d, 2*sizeof(unsigned long long)));
+    const unsigned long long init[2] = {0ull, 0xFFFFFFFFull};
+    HIP_OK(hipMemcpy(d, init, sizeof(init), hipMemcpyHostToDevice));
+    for (uint32_t chunk = 0; chunk < 16; ++chunk)                 // 2^28 inputs per launch
+        k_verify_rcp<<<(1u << 28) / (256*16), 256>>>(chunk << 28, d);
+    HIP_OK(hipGetLastError());
+    unsigned long long h[2];
+    HIP_OK(hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost));
+    (void)hipFree(d);
+    *out_mismatches = h[0];
+    *out_first_bits = (uint32_t)h[1];
+    return RT_OK;
 }
 
 int rt_debug_intersect(rt_scene* s, uint32_t count, const rt_ray_query* rays, int occlusion, rt_hit_record* out) {

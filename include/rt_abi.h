@@ -295,6 +295,12 @@ int rt_debug_mesh_bvh4(const rt_bvh_node* nodes, uint32_t node_count, float* out
 int rt_debug_top_sequences(const rt_bvh_node* nodes, uint32_t node_count, uint32_t index_count,
                            float* out, uint32_t out_cap_entries, uint32_t* out_len);
 
+/* Exhaustive check of the kernels' fast reciprocal (3 instructions instead of the
+ * division expansion) against the correctly rounded IEEE 1.0f / x on `device`: every
+ * one of the 2^32 bit patterns (NaNs compare equal as NaNs).  Writes the number of
+ * mismatching inputs and the smallest mismatching bit pattern (0xFFFFFFFF: none). */
+int rt_debug_verify_rcp(int device, uint64_t* out_mismatches, uint32_t* out_first_bits);
+
 /* The output pass of RT/raytracer.cpp:2103-2171 on the device: per pixel resolve
  * (xyz / w), exposure, 1-exp(-x) tonemap, sRGB power, sigmoidal contrast, x255,
  * TPDF dither from the reference's LDR_RGB1 blue-noise texture number

@@ -311,3 +311,15 @@ def test_atomic_splat_fallback(rt, monkeypatch):
     REPORT["atomic_splat_c1_128"] = {"rel_l2": rel_l2(gpu, cpu)}
     assert (stats.closest_hit_rays, stats.shadow_rays) == (cstats.closest_hit_rays, cstats.shadow_rays)
     assert rel_l2(gpu, cpu) <= 1e-5
+
+
+def test_rcp_cr_exhaustive(rt):
+    """The kernels' 3-instruction reciprocal (rt_dmath.h rcp_cr: v_rcp_f32 + one FMA
+    Newton step, full division outside [2^-125, 2^125]) equals the correctly rounded
+    IEEE 1.0f / x for all 2^32 inputs, so using it in the ray setup, the triangle test
+    and normalize leaves every result bit-identical."""
+    import ctypes as C
+    bad, first = C.c_uint64(), C.c_uint32()
+    assert rt.lib().rt_debug_verify_rcp(0, C.byref(bad), C.byref(first)) == 0
+    REPORT["rcp_cr_exhaustive"] = {"inputs": 1 << 32, "mismatches": bad.value}
+    assert bad.value == 0, f"first mismatch at bits 0x{first.value:08x}"
