@@ -97,6 +97,13 @@ struct DevScene {
 #ifndef RT_LDS_STRATA
 #define RT_LDS_STRATA 0
 #endif
+// RT_PROLOGUE_SCALAR (default): the ray prologue's tables (top-level sequence, leaf
+// records) stay in HBM -- scene_in_lds does not rebase them -- and its wave-uniform
+// walk reads them with s_load through the scalar cache: no LDS round trip and no
+// readfirstlane per value.  ld_uniform's scalar load needs a global address.
+#ifndef RT_PROLOGUE_SCALAR
+#define RT_PROLOGUE_SCALAR 1
+#endif
 enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_TOP_SEQ, BLOB_LEAF_REC,
        BLOB_MESHES, BLOB_STRATA, BLOB_COUNT };
 constexpr uint32_t LDS_SCENE_Q = 2048;   // 32 KB
@@ -119,8 +126,10 @@ RT_D DevScene scene_in_lds(const DevScene& sc, float4* lds) {
     s.inv = reinterpret_cast<const M34*>(b + sc.off[BLOB_INV]);
     s.fwd = reinterpret_cast<const M34*>(b + sc.off[BLOB_FWD]);
     s.lights = reinterpret_cast<const uint32_t*>(b + sc.off[BLOB_LIGHTS]);
+#if !RT_PROLOGUE_SCALAR
     if (sc.top_seq) s.top_seq = reinterpret_cast<const float4*>(b + sc.off[BLOB_TOP_SEQ]);
     s.leaf_rec = reinterpret_cast<const float4*>(b + sc.off[BLOB_LEAF_REC]);
+#endif
     s.meshes = reinterpret_cast<const DevMesh*>(b + sc.off[BLOB_MESHES]);
 #if RT_LDS_STRATA
     s.strata = reinterpret_cast<const uint8_t*>(b + sc.off[BLOB_STRATA]);
@@ -429,12 +438,26 @@ constexpr int FETCH_Q = (RT_MESH_BVH4 ? 8 : (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u
 // (re-testing an analytic primitive at equal t changes nothing: strict tests).
 constexpr uint32_t MLIST_MAX = 4;
 // a load whose address is the same in every active lane, its value moved to SGPRs
+// (RT_PROLOGUE_SCALAR: an s_load through the scalar cache)
 RT_D float4 ld_uniform(const float4* p) {
+#if RT_PROLOGUE_SCALAR
+    // an LDS address here would be a bug (scene_in_lds rebased the table); trap rather
+    // than read a wild global address
+#ifdef __HIP_DEVICE_COMPILE__
+    if (__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p)) __builtin_trap();
+#endif
+    const uint64_t a = (uint64_t)p;
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+    const __attribute__((address_space(4))) float* f = reinterpret_cast<const __attribute__((address_space(4))) float*>(u);
+    return make_float4(f[0], f[1], f[2], f[3]);
+#else
     const float4 v = *p;
     return make_float4(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y))),
                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z))),
                        __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w))));
+#endif
 }
 constexpr uint32_t MLIST_FULL = 0xFFFFFFFFu;
 struct Prologue { float t; uint32_t code; bool occluded, bvh; V3 inv_d; uint32_t mlist; };
