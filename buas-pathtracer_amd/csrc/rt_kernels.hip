@@ -57,6 +57,7 @@ struct DevScene {
     uint32_t air_id;
     const rt_primitive* prims;
     const rt_primitive* planes;
+    const rt_primitive* planes_g;   // the planes in HBM, never rebased (the prologue's scalar loads)
     uint32_t plane_count;
     const M34* inv;                 // per transform: inverse (rows 0-2)
     const M34* fwd;                 // per transform: forward (rows 0-2)
@@ -104,6 +105,7 @@ struct DevScene {
 #ifndef RT_PROLOGUE_SCALAR
 #define RT_PROLOGUE_SCALAR 1
 #endif
+static_assert(sizeof(rt_primitive) == 32 && offsetof(rt_primitive, p) == 16, "the prologue loads a plane's p[] as one float4");
 enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_TOP_SEQ, BLOB_LEAF_REC,
        BLOB_MESHES, BLOB_STRATA, BLOB_COUNT };
 constexpr uint32_t LDS_SCENE_Q = 2048;   // 32 KB
@@ -467,8 +469,13 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
     wr.zero = 0u;                                                  // no pruning on the world ray
     r.t = max_t; r.code = RT_HIT_MISS; r.occluded = false; r.bvh = false; r.inv_d = wr.inv_d; r.mlist = MLIST_FULL;
     for (uint32_t i = 0; i < sc.plane_count; ++i) {
+#if RT_PROLOGUE_SCALAR
+        const float4 pl = ld_uniform(reinterpret_cast<const float4*>(sc.planes_g + i) + 1);   // p[0..3]
+        if (ray_plane(wr, {pl.x, pl.y, pl.z}, pl.w, r.t)) {
+#else
         const rt_primitive& pl = sc.planes[i];
         if (ray_plane(wr, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], r.t)) {
+#endif
             r.code = RT_HIT_PLANE_BIT | i;
             if (occ) { r.occluded = true; return r; }
         }
@@ -2688,6 +2695,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         if (d->lights[i] >= d->primitive_count) { set_error("light id out of range"); return fail(RT_ERROR_INVALID); }
     if ((err = upload(s, d->primitives, d->primitive_count, &ds.prims))) return fail(err);
     if ((err = upload(s, d->planes, d->plane_count, &ds.planes))) return fail(err);
+    ds.planes_g = ds.planes;
     ds.plane_count = d->plane_count;
     std::vector<M34> inv(d->transform_count), fwd(d->transform_count);
     for (uint32_t i = 0; i < d->transform_count; ++i)
