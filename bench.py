@@ -37,6 +37,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table
+L2_PEAK_GBS = 16800.0          # rows gathered from the XCDs' L2, chip-wide (MI355X_MICROARCH.md, lower bound)
 STAGES = ["generate", "extend", "shade", "connect", "splat", "resolve"]
 KERNEL = {"generate": "k_generate", "extend": "k_extend", "shade": "k_shade", "connect": "k_connect",
           "splat": "k_splat", "resolve": "k_resolve"}
@@ -251,6 +252,23 @@ def main():
                             "frac": round(iso_gbs / HBM_PEAK_GBS, 4), "source": tj.get("source")}
         except (OSError, ValueError, KeyError):
             pass
+        # Traversal kernels are bound by dependent L2 / Infinity Cache fetches, not HBM: their
+        # second figure is the bytes each step fetches (profiles/step_stats.json, from an
+        # RT_STEP_STATS build) over the same launch time, against the L2 gather rate
+        # (MI355X_MICROARCH.md, rows shared by every workgroup: 16.8-18.8 TB/s).
+        traversal = None
+        try:
+            with open(os.path.join(ROOT, "profiles", "step_stats.json")) as f:
+                sj = json.load(f)
+            ent = sj.get(KERNEL[dom]) if sj.get("config") == args.config else None
+            if ent and mean_launch_s > 0:
+                tb = ent["steps_per_ray"] * sj["bytes_per_step"] * units_per_launch
+                t_gbs = tb / mean_launch_s / 1e9
+                traversal = {"bytes_per_ray": round(ent["steps_per_ray"] * sj["bytes_per_step"], 1),
+                             "bytes_per_launch": round(tb), "achieved": round(t_gbs, 1), "peak": L2_PEAK_GBS,
+                             "unit": "GB/s", "frac": round(t_gbs / L2_PEAK_GBS, 4), "source": sj.get("source")}
+        except (OSError, ValueError, KeyError):
+            pass
         ref = wms if args.warmup else [x / args.steps for x in kms]        # all stages: warm-up frames
         concurrency = sum(ref[:5]) / (elapsed * 1e3 / args.steps) if elapsed > 0 else 0.0
         pipe_bytes = PIPE_BYTES_PER_RAY * (closest + shadow) + PIPE_BYTES_PER_SAMPLE * samples
@@ -304,7 +322,7 @@ def main():
                          "kernel": KERNEL[dom], "bytes_per_unit": BYTES_PER_UNIT[dom],
                          "units_per_launch": round(units_per_launch, 1),
                          "mean_launch_ms": round(mean_launch_s * 1e3, 4),
-                         "concurrency": round(concurrency, 2), "isolated": isolated,
+                         "concurrency": round(concurrency, 2), "isolated": isolated, "traversal": traversal,
                          "pipeline": {"bytes": pipe_bytes, "achieved": round(pipe_gbs, 1),
                                       "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),
                                       "formula": "152 B x (closest + shadow rays) + 144 B x samples, rank 0, / wall time"}},
