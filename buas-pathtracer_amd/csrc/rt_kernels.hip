@@ -1062,6 +1062,29 @@ RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float
 // ======================================================================
 // Path pool (SoA in HBM)
 // ======================================================================
+// Streaming access to the path pool, the queues and the sample records: each is read
+// or written once per iteration (hundreds of MB per launch, no reuse before the next
+// iteration), so with RT_NT_POOL they use non-temporal loads and stores and do not
+// displace the BVH nodes and triangles the trace kernels keep re-reading from L2.
+#ifndef RT_NT_POOL
+#define RT_NT_POOL 1
+#endif
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
+typedef float nt_f2 __attribute__((ext_vector_type(2)));
+#if RT_NT_POOL
+RT_D float4 ldnt(const float4* p) { const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p)); return make_float4(v.x, v.y, v.z, v.w); }
+RT_D uint4 ldnt(const uint4* p) { const nt_u4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_u4*>(p)); return make_uint4(v.x, v.y, v.z, v.w); }
+RT_D float2 ldnt(const float2* p) { const nt_f2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f2*>(p)); return make_float2(v.x, v.y); }
+RT_D float ldnt(const float* p) { return __builtin_nontemporal_load(p); }
+RT_D void stnt(float4* p, float4 v) { const nt_f4 t = {v.x, v.y, v.z, v.w}; __builtin_nontemporal_store(t, reinterpret_cast<nt_f4*>(p)); }
+RT_D void stnt(uint4* p, uint4 v) { const nt_u4 t = {v.x, v.y, v.z, v.w}; __builtin_nontemporal_store(t, reinterpret_cast<nt_u4*>(p)); }
+RT_D void stnt(float2* p, float2 v) { const nt_f2 t = {v.x, v.y}; __builtin_nontemporal_store(t, reinterpret_cast<nt_f2*>(p)); }
+RT_D void stnt(float* p, float v) { __builtin_nontemporal_store(v, p); }
+#else
+template <typename T> RT_D T ldnt(const T* p) { return *p; }
+template <typename T> RT_D void stnt(T* p, T v) { *p = v; }
+#endif
 struct Pool {
     uint32_t n;
     float4* ray_o;       // o.xyz | w: pixel index bits
@@ -1549,16 +1572,16 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
         if (OCC) {
             if (!tr.occluded) {
                 const uint32_t slot = pool.sh_slot[item];
-                const float4 c = pool.sh_c[item];
-                float4 L = pool.L[slot];
+                const float4 c = ldnt(&pool.sh_c[item]);
+                float4 L = ldnt(&pool.L[slot]);
                 L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;   // total_color += ... (:768)
-                pool.L[slot] = L;
+                stnt(&pool.L[slot], L);
             }
         } else if (tr.code != RT_HIT_MISS) {                  // a BVH hit; else k_shade's plane result stands
             const uint32_t slot = item;                       // the path's slot (from the record)
             const Hit h = tr.result();
-            pool.hit[slot] = make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v);
-            pool.hit_w[slot] = h.w;
+            stnt(&pool.hit[slot], make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v));
+            stnt(&pool.hit_w[slot], h.w);
         }
     };
     for (;;) {
@@ -1591,7 +1614,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             if (!active && rank < avail) {
                 item = chunk_next + rank;
                 const float4* q = (OCC ? pool.sh_rec : pool.ext_rec[cur]) + REC_Q*(size_t)item;
-                const float4 o = q[0], d = q[1], iv = q[2];
+                const float4 o = ldnt(&q[0]), d = ldnt(&q[1]), iv = ldnt(&q[2]);
                 if (!OCC) item = __float_as_uint(o.w);            // the path's slot
                 tr.init_rec(sc, st, ld3(o), ld3(d), ld3(iv), d.w, OCC ? __float_as_uint(o.w) : 0u, __float_as_uint(iv.w));
                 steps = 0;
@@ -1653,10 +1676,10 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     uint32_t sh_light = 0;
     if (valid) {
         SP_MARK(t_load);
-        const float4 o4 = pool.ray_o[slot], d4 = pool.ray_d[slot];
-        const float4 t4 = pool.thr[slot], L4 = pool.L[slot], pn4 = pool.prev_n[slot];
-        const float4 h4 = pool.hit[slot];
-        const uint4 r4 = pool.rng[slot];
+        const float4 o4 = ldnt(&pool.ray_o[slot]), d4 = ldnt(&pool.ray_d[slot]);
+        const float4 t4 = ldnt(&pool.thr[slot]), L4 = ldnt(&pool.L[slot]), pn4 = ldnt(&pool.prev_n[slot]);
+        const float4 h4 = ldnt(&pool.hit[slot]);
+        const uint4 r4 = ldnt(&pool.rng[slot]);
         Rng rng = {r4.x, r4.y, r4.z, r4.w};
         V3 ro = ld3(o4), rd = ld3(d4);
         V3 thr = ld3(t4), total = ld3(L4), prev_N = ld3(pn4);
@@ -1669,7 +1692,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         uint32_t canonical = fp.frame_count + (fp.list_xy ? fp.list_s[sample_off] : sample_off);
         SamplerState ss = {px, py, canonical, st.sampling_strategy};
         Hit h;
-        h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = pool.hit_w[slot];
+        h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = ldnt(&pool.hit_w[slot]);
         Ray ray; ray.o = ro; ray.d = rd;
         SP_ADD(SP_LOAD, t_load);
         if (h.code != RT_HIT_MISS) {
@@ -1839,18 +1862,18 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         if (cont) {                                        // next bounce's intersect_scene: planes + top level here
             SP_MARK(t_cpro);
             cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
-            pool.hit[slot] = make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f);
-            pool.hit_w[slot] = 0.0f;
+            stnt(&pool.hit[slot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
+            stnt(&pool.hit_w[slot], 0.0f);
             enq = cpro.bvh;
             SP_ADD(SP_CPRO, t_cpro);
         }
         SP_MARK(t_store);
-        pool.ray_o[slot] = make_float4(ro.x, ro.y, ro.z, o4.w);
-        pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, d4.w);
-        pool.thr[slot] = make_float4(thr.x, thr.y, thr.z, t4.w);
-        pool.L[slot] = make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at)));
-        pool.prev_n[slot] = make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w);
-        pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
+        stnt(&pool.ray_o[slot], make_float4(ro.x, ro.y, ro.z, o4.w));
+        stnt(&pool.ray_d[slot], make_float4(rd.x, rd.y, rd.z, d4.w));
+        stnt(&pool.thr[slot], make_float4(thr.x, thr.y, thr.z, t4.w));
+        stnt(&pool.L[slot], make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
+        stnt(&pool.prev_n[slot], make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w));
+        stnt(&pool.rng[slot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
         SP_ADD(SP_STORE, t_store);
     }
     SP_MARK(t_tail);
@@ -1869,18 +1892,18 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const uint32_t pos = tpos[0];
     if (enq) {
         float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + pos);
-        q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
-        q[1] = make_float4(nrd.x, nrd.y, nrd.z, cpro.t);
-        q[2] = make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, __uint_as_float(cpro.mlist));
+        stnt(&q[0], make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot)));
+        stnt(&q[1], make_float4(nrd.x, nrd.y, nrd.z, cpro.t));
+        stnt(&q[2], make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, __uint_as_float(cpro.mlist)));
     }
     const uint32_t spos = shard*pool.shard_cap + tpos[1];
     if (shadow) {
         pool.sh_slot[spos] = slot;
         float4* q = pool.sh_rec + REC_Q*(size_t)spos;
-        q[0] = make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light));
-        q[1] = make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t);
-        q[2] = make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist));
-        pool.sh_c[spos] = make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f);
+        stnt(&q[0], make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light)));
+        stnt(&q[1], make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t));
+        stnt(&q[2], make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist)));
+        stnt(&pool.sh_c[spos], make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f));
     }
     if (done) pool.state[slot] = S_DONE;
     if (threadIdx.x == 0) pool.free_n[blockIdx.x] = ttot[5];
