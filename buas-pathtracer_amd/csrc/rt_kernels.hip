@@ -1069,6 +1069,9 @@ RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float
 #ifndef RT_NT_POOL
 #define RT_NT_POOL 1
 #endif
+#ifndef RT_NT_SPLAT
+#define RT_NT_SPLAT 1
+#endif
 typedef float nt_f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
 typedef float nt_f2 __attribute__((ext_vector_type(2)));
@@ -1350,8 +1353,13 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
         } else if (fp.samp_rgbx) {
             // deterministic path: store the sample; k_resolve gathers it in reference order
             const size_t rec = (size_t)__float_as_uint(pool.ray_d[slot].w)*fp.pixels + __float_as_uint(pool.prev_n[slot].w);
+#if RT_NT_SPLAT
+            stnt(&fp.samp_rgbx[rec], make_float4(r.x, r.y, r.z, j.x));      // read again only by k_resolve
+            stnt(&fp.samp_jy[rec], j.y);
+#else
             fp.samp_rgbx[rec] = make_float4(r.x, r.y, r.z, j.x);
             fp.samp_jy[rec] = j.y;
+#endif
         } else if (fp.cache_size) {
             const int64_t x = pixel % fp.w, y = pixel / fp.w;
             const int64_t ks = fp.kernel_size;
