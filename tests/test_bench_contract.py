@@ -1,0 +1,45 @@
+"""bench.py's contract pieces that need no GPU: the constants the JSON line is built
+from and the measured tables it reads (profiles/traffic.json from the rocprofv3 --pmc
+passes, profiles/step_stats.json from an RT_STEP_STATS build) have the shape bench.py
+expects, so a round-end bench run on a fresh box cannot lose its roofline block."""
+import importlib.util
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)            # module level only: main() is behind __main__
+    return mod
+
+
+def test_stage_tables_agree(bench):
+    assert set(bench.BYTES_PER_UNIT) <= set(bench.STAGES)
+    assert set(bench.KERNEL) >= set(bench.BYTES_PER_UNIT)
+    assert bench.BYTES_PER_UNIT["shade"] == 192
+    assert bench.HBM_PEAK_GBS == 8000.0 and bench.L2_PEAK_GBS > bench.HBM_PEAK_GBS
+    assert "c3" in bench.CONFIGS
+
+
+def test_traffic_table(bench):
+    tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
+    assert tj["config"] == "c3"
+    for stage in ("generate", "extend", "shade", "connect"):
+        ent = tj["kernels"][bench.KERNEL[stage]]
+        assert ent["hbm_bytes_per_launch"] > 0 and ent["isolated_mean_us"] > 0
+        assert ent["dispatches"] >= 1
+
+
+def test_step_stats_table(bench):
+    sj = json.load(open(os.path.join(ROOT, "profiles", "step_stats.json")))
+    assert sj["config"] == "c3" and sj["bytes_per_step"] == 128
+    for k in ("k_extend", "k_connect"):
+        e = sj[k]
+        assert e["steps_per_ray"] >= e["interior_per_ray"] + e["leaf_per_ray"] > 0
+        assert 0.0 < e["simd_efficiency"] <= 1.0
