@@ -323,7 +323,8 @@ int rt_set_profiling(int enable);
  * record no events, so their launches are not slowed by the markers). */
 int rt_set_profiling_stages(uint32_t mask);
 
-/* Size of the in-flight path pool (paths resident in HBM); 0 = default (2^21). */
+/* Size of the in-flight path pool per partition (paths resident in HBM); 0 = default:
+ * an eighth of the partition's samples, clamped to [2^21, 3 x 2^21]. */
 int rt_set_path_pool(uint32_t paths);
 
 /* discard_current_render (RT/raytracer.cpp:686-690): polled between wavefront
