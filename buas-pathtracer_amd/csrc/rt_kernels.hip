@@ -1069,6 +1069,9 @@ RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float
 #ifndef RT_NT_POOL
 #define RT_NT_POOL 1
 #endif
+#ifndef RT_DONE_SLIM
+#define RT_DONE_SLIM 1      // k_shade writes only L (vignette in .w) for a path that finishes
+#endif
 #ifndef RT_NT_SPLAT
 #define RT_NT_SPLAT 1
 #endif
@@ -1342,10 +1345,9 @@ constexpr int EV_SLOTS = 8;     // iterations in flight per partition in run_fra
 RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
     {
         const float4 L = pool.L[slot];
-        const float vig = pool.thr[slot].w;
+        const float vig = RT_DONE_SLIM ? L.w : pool.thr[slot].w;     // k_shade / k_generate put it in L.w
         const float2 j = pool.jitter[slot];
         V3 r = muls(ld3(L), vig);
-        const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
         if (fp.list_xy) {
             const uint32_t k = __float_as_uint(pool.ray_d[slot].w);
             float* o = fp.list_out + 5*(size_t)k;
@@ -1361,6 +1363,7 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
             fp.samp_jy[rec] = j.y;
 #endif
         } else if (fp.cache_size) {
+            const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
             const int64_t x = pixel % fp.w, y = pixel / fp.w;
             const int64_t ks = fp.kernel_size;
             const float kscale = (float)(fp.cache_size - 1) / (float)ks;
@@ -1384,6 +1387,7 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
                 }
             }
         } else {
+            const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
             float* dst = reinterpret_cast<float*>(fp.accum + pixel);
             unsafeAtomicAdd(dst + 0, r.x);
             unsafeAtomicAdd(dst + 1, r.y);
@@ -1481,12 +1485,12 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         pool.ray_o[slot] = make_float4(jcp.x, jcp.y, jcp.z, __uint_as_float(y*fp.w + x));
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
         pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
-        pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(pack_flags(0, 1, 0)));
+        cast = st.max_bounce_count > 0;
+        pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, (RT_DONE_SLIM && !cast) ? vig : __uint_as_float(pack_flags(0, 1, 0)));
         pool.prev_n[slot] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(p));
         pool.jitter[slot] = make_float2(jx, jy);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         pool.mstack[slot] = (uint16_t)sc.air_id;            // material_stack[0] = &air
-        cast = st.max_bounce_count > 0;
         pool.state[slot] = cast ? S_TRACE : S_DONE;      // max_bounce_count == 0: nothing to trace
         if (cast) {
             pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false, 0u);
@@ -1876,12 +1880,27 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             SP_ADD(SP_CPRO, t_cpro);
         }
         SP_MARK(t_store);
+#if RT_DONE_SLIM
+        // A finished path is only splatted: the next k_generate reads L (with the vignette
+        // in .w instead of the flags), the jitter and the .w words of ray_d / prev_n, which
+        // never change.  Its ray, throughput, normal and RNG state are not written back.
+        stnt(&pool.L[slot], make_float4(total.x, total.y, total.z,
+                                        done ? t4.w : __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
+        if (!done) {
+            stnt(&pool.ray_o[slot], make_float4(ro.x, ro.y, ro.z, o4.w));
+            stnt(&pool.ray_d[slot], make_float4(rd.x, rd.y, rd.z, d4.w));
+            stnt(&pool.thr[slot], make_float4(thr.x, thr.y, thr.z, t4.w));
+            stnt(&pool.prev_n[slot], make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w));
+            stnt(&pool.rng[slot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
+        }
+#else
         stnt(&pool.ray_o[slot], make_float4(ro.x, ro.y, ro.z, o4.w));
         stnt(&pool.ray_d[slot], make_float4(rd.x, rd.y, rd.z, d4.w));
         stnt(&pool.thr[slot], make_float4(thr.x, thr.y, thr.z, t4.w));
         stnt(&pool.L[slot], make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
         stnt(&pool.prev_n[slot], make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w));
         stnt(&pool.rng[slot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
+#endif
         SP_ADD(SP_STORE, t_store);
     }
     SP_MARK(t_tail);
