@@ -1490,7 +1490,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         pool.prev_n[slot] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(p));
         pool.jitter[slot] = make_float2(jx, jy);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
-        pool.mstack[slot] = (uint16_t)sc.air_id;            // material_stack[0] = &air
+        // material_stack[0] = &air: level 0 is never stored; k_shade reads it as sc.air_id
         pool.state[slot] = cast ? S_TRACE : S_DONE;      // max_bounce_count == 0: nothing to trace
         if (cast) {
             pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false, 0u);
@@ -1718,11 +1718,12 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             uint32_t mi_id, mt_id;
             if (inside) {
                 mi_id = surf_id;
-                mt_id = pool.mstack[(size_t)(at - 1 > 0 ? at - 1 : 0)*pool.n + slot];
+                const int32_t lv = at - 1 > 0 ? at - 1 : 0;
+                mt_id = lv ? pool.mstack[(size_t)lv*pool.n + slot] : sc.air_id;     // level 0 = air
                 cos_i = -cos_i;
                 N = neg(N);
             } else {
-                mi_id = pool.mstack[(size_t)at*pool.n + slot];
+                mi_id = at ? pool.mstack[(size_t)at*pool.n + slot] : sc.air_id;
                 mt_id = surf_id;
             }
             const rt_material mi = sc.materials[mi_id];
