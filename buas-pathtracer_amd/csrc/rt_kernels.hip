@@ -1676,9 +1676,21 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     unsigned long long prof[SP_N] = {};
     SP_MARK(t_start);
 #endif
-    const DevScene sc = scene_in_lds(sc_g, lds_scene);
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
-    const uint8_t state0 = slot < pool.n ? pool.state[slot] : (uint8_t)S_FREE;
+    // The slot's state and path record are loaded before the scene copy, whatever the
+    // state: the three round trips (state, record, LDS blob) overlap instead of running
+    // back to back.  A slot not traced this iteration (~1/6 of the pool) reads 120 B for nothing.
+    uint8_t state0 = S_FREE;
+    float4 o4 = {}, d4 = {}, t4 = {}, L4 = {}, pn4 = {}, h4 = {};
+    uint4 r4 = {};
+    float hw = 0.0f;
+    if (slot < pool.n) {
+        state0 = pool.state[slot];
+        o4 = ldnt(&pool.ray_o[slot]); d4 = ldnt(&pool.ray_d[slot]);
+        t4 = ldnt(&pool.thr[slot]); L4 = ldnt(&pool.L[slot]); pn4 = ldnt(&pool.prev_n[slot]);
+        h4 = ldnt(&pool.hit[slot]); r4 = ldnt(&pool.rng[slot]); hw = ldnt(&pool.hit_w[slot]);
+    }
+    const DevScene sc = scene_in_lds(sc_g, lds_scene);
     const bool valid = slot < pool.n && state0 == S_TRACE;             // traced this iteration
     bool cont = false, done = false, shadow = false, cast_shadow = false, enq = false;
     Prologue spro = {}, cpro = {};
@@ -1688,10 +1700,6 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     uint32_t sh_light = 0;
     if (valid) {
         SP_MARK(t_load);
-        const float4 o4 = ldnt(&pool.ray_o[slot]), d4 = ldnt(&pool.ray_d[slot]);
-        const float4 t4 = ldnt(&pool.thr[slot]), L4 = ldnt(&pool.L[slot]), pn4 = ldnt(&pool.prev_n[slot]);
-        const float4 h4 = ldnt(&pool.hit[slot]);
-        const uint4 r4 = ldnt(&pool.rng[slot]);
         Rng rng = {r4.x, r4.y, r4.z, r4.w};
         V3 ro = ld3(o4), rd = ld3(d4);
         V3 thr = ld3(t4), total = ld3(L4), prev_N = ld3(pn4);
@@ -1704,7 +1712,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         uint32_t canonical = fp.frame_count + (fp.list_xy ? fp.list_s[sample_off] : sample_off);
         SamplerState ss = {px, py, canonical, st.sampling_strategy};
         Hit h;
-        h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = ldnt(&pool.hit_w[slot]);
+        h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = hw;
         Ray ray; ray.o = ro; ray.d = rd;
         SP_ADD(SP_LOAD, t_load);
         if (h.code != RT_HIT_MISS) {
