@@ -1413,7 +1413,6 @@ __global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out
 __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                     Counters* cnt, int cur) {
     __shared__ uint32_t agg[BLOCK / 64 + 1];
-    const DevScene sc = scene_in_lds(sc_g, lds_scene);
     // Free slots claim consecutive sample numbers in slot order: the block's first
     // claim is the scan of the free counts k_bookkeep made (no atomics).  The block's
     // free slots are handed to its first nfree threads (slot order kept), so the waves
@@ -1425,6 +1424,9 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         splat_sample(fp, pool, own);
         pool.state[own] = S_FREE;                // a claim below may reuse the slot (ordered by the barrier)
     }
+    // No sample left for this block to claim (the frame's drain): splat only, no scene copy
+    if ((unsigned long long)pool.claim_base[blockIdx.x] >= remaining_samples(cnt)) return;
+    const DevScene sc = scene_in_lds(sc_g, lds_scene);
     const bool own_free = own_state != S_TRACE;
     uint32_t nfree;
     const uint32_t rank = block_rank<BLOCK>(own_free, agg, &nfree);
