@@ -1528,7 +1528,10 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
 #define RT_TB 256
 #endif
 constexpr int TB = RT_TB;
-constexpr uint32_t CHUNK = 256;
+#ifndef RT_CHUNK
+#define RT_CHUNK 256
+#endif
+constexpr uint32_t CHUNK = RT_CHUNK;
 #ifndef RT_STEPS_PER_REFILL
 #define RT_STEPS_PER_REFILL 8
 #endif
