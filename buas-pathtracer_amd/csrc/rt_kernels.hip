@@ -2981,6 +2981,14 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         int per_cu = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
+        // Persistent trace blocks: 75 % of one full-occupancy wave of blocks (RT_TRACE_GRID_PCT).
+        // Four partitions run their trace launches side by side; a full grid per launch left
+        // less room for the other partitions' generate / shade blocks.  C3 A/B, 5 alternating
+        // pairs: 75 % +1.5 %, 60 % +0.9 %, 50 % +1.5 % (2 pairs), 150 % -0.8 %.  The spill
+        // area is sized from the result.
+        int grid_pct = 75;
+        if (const char* e = getenv("RT_TRACE_GRID_PCT")) grid_pct = std::max(1, atoi(e));
+        s->trace_grid = std::max(1u, (uint32_t)((unsigned long long)s->trace_grid*(unsigned)grid_pct / 100ull));
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
