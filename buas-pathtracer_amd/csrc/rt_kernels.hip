@@ -1977,15 +1977,26 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
 // RES_RY pixels, 60 instead of 200 at r = 2).  The 64 lanes of a wave own 64
 // adjacent columns, so at every step they read 64 adjacent records of one
 // sample plane (record = s*P + p): the loads stay coalesced.
+// Strip height: 8 rows when the shard owns at least RES_TALL_PIXELS pixels, else 4.  Taller
+// strips read fewer records per pixel ((8 + 4)/8 against (4 + 4)/4 source rows) but make half
+// as many threads: the full C3 frame resolves in 21.7 ms instead of 24.0 (frame +1.2 %, A/B
+// twice), one rank's eighth in 9.8 ms instead of 5.5 (too few waves to cover the latency).
 #ifndef RT_RES_RY
 #define RT_RES_RY 4
 #endif
-constexpr int RES_RY = RT_RES_RY;      // 4: measured best of 2, 4, 6, 8, 16 (C3 256 spp: 30 ms)
+#ifndef RT_RES_RY_TALL
+#define RT_RES_RY_TALL 8
+#endif
+#ifndef RT_RES_TALL_PIXELS
+#define RT_RES_TALL_PIXELS 1600000u
+#endif
+constexpr uint32_t RES_TALL_PIXELS = RT_RES_TALL_PIXELS;
 #ifndef RT_RES_U
 #define RT_RES_U 8
 #endif
 constexpr int RES_U = RT_RES_U;        // sample records loaded ahead per thread
 constexpr int RES_BX = 64, RES_BY = 4;
+template <int RES_RY>
 __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
     __shared__ float lut[512];
     for (int i = threadIdx.x; i < 512; i += RES_BX*RES_BY) lut[i] = fp.cache_size ? fp.lut[i] : 0.0f;
@@ -3167,8 +3178,11 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool prof_resolve = (g_profiling >> RT_KERNEL_RESOLVE) & 1u;
     if (prof_resolve) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
-    dim3 rgrid((w + RES_BX - 1) / RES_BX, (h + RES_BY*RES_RY - 1) / (RES_BY*RES_RY));
-    k_resolve<<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
+    const bool tall = fp.pixels >= RES_TALL_PIXELS;
+    const int rry = tall ? RT_RES_RY_TALL : RT_RES_RY;
+    dim3 rgrid((w + RES_BX - 1) / RES_BX, (h + RES_BY*rry - 1) / (RES_BY*rry));
+    if (tall) k_resolve<RT_RES_RY_TALL><<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
+    else k_resolve<RT_RES_RY><<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
     HIP_OK(hipGetLastError());
     if (prof_resolve) HIP_OK(hipEventRecord(e1, stream));
     HIP_OK(hipStreamSynchronize(stream));
