@@ -16,7 +16,7 @@ def main():
     ap.add_argument("--bucket-ms", type=float, default=5.0)
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace)) if r["Kernel_Name"].startswith(("k_", "void k_"))]
-    ri = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_resolve")]
+    ri = [i for i, r in enumerate(rows) if "k_resolve" in r["Kernel_Name"]]
     if len(ri) < 2:
         raise SystemExit("need two frames (two k_resolve launches) in the trace")
     fr = rows[ri[0] + 1:ri[1] + 1]
@@ -33,7 +33,7 @@ def main():
             s, b = be, b + 1
     print(f"frame {(t1 - t0) / 1e6:.1f} ms; kernels in flight per {a.bucket_ms:g} ms:")
     print(" ".join(f"{x / bucket:.1f}" for x in busy))
-    res = next(r for r in fr if r["Kernel_Name"].startswith("k_resolve"))
+    res = next(r for r in fr if "k_resolve" in r["Kernel_Name"])
     print(f"resolve {(int(res['Start_Timestamp']) - t0) / 1e6:.1f} -> {(int(res['End_Timestamp']) - t0) / 1e6:.1f} ms")
 
 
