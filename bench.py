@@ -171,12 +171,15 @@ def main():
         return dev.render_device(cam, st, fc, w, h, buf.data_ptr(), stream=stream.cuda_stream,
                                  shard_index=shard_index, shard_count=shard_count)
 
+    scratch = torch.zeros_like(accum) if world > 1 else None
+
     def step():
         accum.zero_()
         if args.shard_of > 1:                          # diagnostic: rank 0's share of an N-rank frame
             return render_shard(0, args.shard_of, accum)
-        # tiles t % world == rank, then the RCCL sum-reduce of the framebuffer over xGMI
-        return render_frame_sharded(render_shard, accum, rank, world)
+        # tiles t % world == rank into a zeroed frame buffer, the RCCL sum-reduce of it over
+        # xGMI into rank 0, which adds it to its accumulation buffer
+        return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch)
 
     # Warm-up frames time every stage (HIP events around each launch); the timed region
     # then records events for the dominant stage only, since each event pair is a queue

@@ -26,7 +26,8 @@ from .abi import (V3, v3, M4x4Inv, Material, Camera, Settings, FilterCache, Post
 
 __all__ = ["Scene", "DeviceScene", "RenderError", "load_preset", "default_settings", "load_reconstruction_kernel",
            "translate", "scale", "rotate_x", "rotate_y", "rotate_z", "identity", "aim_camera", "aim_camera_at",
-           "recompute_camera", "resolve_bgra8", "postprocess", "write_bitmap", "lib", "abi", "v3", "PI_32", "DEG_TO_RAD"]
+           "recompute_camera", "resolve_bgra8", "postprocess", "write_bitmap", "lib", "abi", "v3", "PI_32", "DEG_TO_RAD",
+           "set_splat_mode", "splat_mode", "take_picture", "read_bitmap"]
 
 PI_32 = 3.14159265359
 DEG_TO_RAD = 6.28318530717 / 360.0
@@ -298,6 +299,44 @@ def write_bitmap(path, bgra):
     b = np.ascontiguousarray(bgra, np.uint32)
     if not lib().rth_write_bitmap(str(path).encode(), b.ctypes.data_as(C.POINTER(C.c_uint32)), w, h):
         raise OSError(lib().rth_last_error().decode())
+
+
+def set_splat_mode(mode):
+    """rt_set_splat_mode: abi.RT_SPLAT_STREAM (default), RT_SPLAT_EXACT (the reference's splat
+    order, bit-identical frames) or RT_SPLAT_ATOMIC."""
+    _check(lib().rt_set_splat_mode(int(mode)))
+
+
+class splat_mode:
+    """with splat_mode(abi.RT_SPLAT_EXACT): ... restores the default (streaming) splat after."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        set_splat_mode(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_splat_mode(abi.RT_SPLAT_STREAM)
+        return False
+
+
+def read_bitmap(path, w, h):
+    """The BGRA8 pixels (h, w) u32 of a bitmap write_bitmap wrote."""
+    out = np.zeros((h, w), np.uint32)
+    if not lib().rth_read_bitmap(str(path).encode(), out.ctypes.data_as(C.POINTER(C.c_uint32)), w, h):
+        raise OSError(lib().rth_last_error().decode())
+    return out
+
+
+def take_picture(scene, camera, settings, filter_cache, post, w, h, spp, path, total_frame_index=0, device=0):
+    """rth_take_picture: the reference's "Take picture" (RT/raytracer.cpp:2031-2185) -> BMP at `path`."""
+    stats = Stats()
+    _check(lib().rth_take_picture(scene.handle, C.byref(camera), C.byref(settings), C.byref(filter_cache),
+                                  C.byref(post), w, h, spp, total_frame_index, device, str(path).encode(),
+                                  C.byref(stats)))
+    return stats
 
 
 def device_count():

@@ -24,6 +24,7 @@ RT_MATERIAL_EMISSIVE = 0x4
 
 RT_PRIMITIVE_NONE, RT_PRIMITIVE_PLANE, RT_PRIMITIVE_SPHERE, RT_PRIMITIVE_BOX, RT_PRIMITIVE_MESH = range(5)
 RT_SAMPLING_UNIFORM, RT_SAMPLING_OPTIMIZED_BLUE_NOISE, RT_SAMPLING_STRATIFIED = range(3)
+RT_SPLAT_STREAM, RT_SPLAT_EXACT, RT_SPLAT_ATOMIC = range(3)          # rt_splat_mode
 RT_RNG_PER_SAMPLE, RT_RNG_TILE_STREAM = 0, 1
 RT_HIT_MISS = 0xFFFFFFFF
 RT_HIT_PLANE_BIT = 0x80000000
@@ -124,14 +125,14 @@ class Stats(C.Structure):
     _fields_ = [("closest_hit_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
                 ("iterations", C.c_uint64), ("seconds", C.c_double),
                 ("kernel_ms", C.c_double * RT_KERNEL_COUNT), ("kernel_launches", C.c_uint64 * RT_KERNEL_COUNT),
-                ("traced_rays", C.c_uint64 * 2)]
+                ("traced_rays", C.c_uint64 * 2), ("splat_mode", C.c_int32), ("reserved", C.c_int32)]
 
     def as_dict(self):
         return {"closest_hit_rays": self.closest_hit_rays, "shadow_rays": self.shadow_rays,
                 "samples": self.samples, "iterations": self.iterations, "seconds": self.seconds,
                 "kernel_ms": {RT_KERNEL_NAMES[i]: self.kernel_ms[i] for i in range(6)},
                 "kernel_launches": {RT_KERNEL_NAMES[i]: self.kernel_launches[i] for i in range(6)},
-                "traced_rays": [self.traced_rays[0], self.traced_rays[1]]}
+                "traced_rays": [self.traced_rays[0], self.traced_rays[1]], "splat_mode": self.splat_mode}
 
 
 class RayQuery(C.Structure):
@@ -177,6 +178,9 @@ ABI_FUNCTIONS = {
     "rt_set_profiling": (C.c_int, [C.c_int]),
     "rt_set_profiling_stages": (C.c_int, [C.c_uint32]),
     "rt_set_path_pool": (C.c_int, [C.c_uint32]),
+    "rt_set_splat_mode": (C.c_int, [C.c_int]),
+    "rt_render_picture": (C.c_int, [C.c_void_p, P(Camera), P(Settings), P(FilterCache), P(TileSet), C.c_uint32,
+                                    C.c_uint32, C.c_uint32, P(PostSettings), P(C.c_uint32), P(Stats)]),
     "rt_cancel": (C.c_int, [C.c_void_p]),
     "rt_postprocess_device": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, P(PostSettings), C.c_uint32,
                                         C.c_void_p, C.c_void_p]),
@@ -223,7 +227,8 @@ HOST_FUNCTIONS = {
     "rth_resolve_bgra8": (None, [P(AccumulationBuffer), P(PostSettings), P(C.c_uint32)]),
     "rth_write_bitmap": (C.c_int, [C.c_char_p, P(C.c_uint32), C.c_uint32, C.c_uint32]),
     "rth_take_picture": (C.c_int, [C.c_void_p, P(Camera), P(Settings), P(FilterCache), P(PostSettings),
-                                   C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_char_p, P(Stats)]),
+                                   C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_char_p, P(Stats)]),
+    "rth_read_bitmap": (C.c_int, [C.c_char_p, P(C.c_uint32), C.c_uint32, C.c_uint32]),
 }
 
 

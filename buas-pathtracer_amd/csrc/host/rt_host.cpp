@@ -1027,4 +1027,18 @@ int rth_write_bitmap(const char* path, const uint32_t* px, uint32_t w, uint32_t 
     return 1;
 }
 
+int rth_read_bitmap(const char* path, uint32_t* px, uint32_t w, uint32_t h) {   // the layout write_bitmap writes
+    FILE* f = fopen(path, "rb");
+    if (!f) { set_err(std::string("cannot open ") + path); return 0; }
+    unsigned char hd[54];
+    int ok = fread(hd, 1, sizeof(hd), f) == sizeof(hd);
+    uint32_t off = 0; int32_t bw = 0, bh = 0; uint16_t bpp = 0;
+    if (ok) { memcpy(&off, hd + 10, 4); memcpy(&bw, hd + 18, 4); memcpy(&bh, hd + 22, 4); memcpy(&bpp, hd + 28, 2); }
+    ok = ok && hd[0] == 'B' && hd[1] == 'M' && bpp == 32 && bw == (int32_t)w && bh == -(int32_t)h &&
+         fseek(f, (long)off, SEEK_SET) == 0 && fread(px, 4, (size_t)w*h, f) == (size_t)w*h;
+    fclose(f);
+    if (!ok) set_err(std::string("not a top-down 32-bit bitmap of the expected size: ") + path);
+    return ok;
+}
+
 }  // extern "C"

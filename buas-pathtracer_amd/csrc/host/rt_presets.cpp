@@ -425,22 +425,24 @@ extern "C" int rth_load_preset(const char* name_c, uint32_t w, uint32_t h, const
 
 extern "C" int rth_take_picture(rth_scene* s, const rt_camera* camera, const rt_settings* settings,
                                 const rt_filter_cache* filter, const rth_post_settings* post,
-                                uint32_t w, uint32_t h, uint32_t spp, int device, const char* bmp_path,
-                                rt_stats* stats_out) {
+                                uint32_t w, uint32_t h, uint32_t spp, uint32_t total_frame_index, int device,
+                                const char* bmp_path, rt_stats* stats_out) {
+    // "Take picture" (RT/raytracer.cpp:2037-2041): discard the render, samples_per_pixel = picture_spp;
+    // render_all_tiles renders the frame, the output pass dithers it into BGRA8 (:2103-2173) and
+    // write_bitmap stores it (:2175-2179, RT/assets.cpp:693-724).  The frame and its output pass run
+    // on the device (rt_render_picture); only the BGRA8 picture comes back.
     rt_scene* dev = nullptr;
     int err = rt_scene_upload(rth_scene_desc(s), device, &dev);
     if (err) return err;
     rt_settings st = *settings;
     st.samples_per_pixel = spp;
-    std::vector<float> px((size_t)w*h*4, 0.0f);
-    rt_accumulation_buffer acc = {w, h, 0, px.data()};
     rt_tile_set tiles = {64, 64, 0, 1};
+    rt_post_settings pp = {post->exposure, post->tonemapping, post->srgb_transform, post->midpoint, post->contrast};
     rt_stats stats = {};
-    err = rt_render(dev, camera, &st, filter, &tiles, 0, &acc, &stats);
+    std::vector<uint32_t> bgra((size_t)w*h);
+    err = rt_render_picture(dev, camera, &st, filter, &tiles, total_frame_index, w, h, &pp, bgra.data(), &stats);
     rt_scene_free(dev);
     if (err) return err;
-    std::vector<uint32_t> bgra((size_t)w*h);
-    rth_resolve_bgra8(&acc, post, bgra.data());
     if (!rth_write_bitmap(bmp_path, bgra.data(), w, h)) return RT_ERROR_INVALID;
     printf("Took %ux%u %uspp image in %f seconds.\n", w, h, spp, stats.seconds);   // :2177-2179
     if (stats_out) *stats_out = stats;

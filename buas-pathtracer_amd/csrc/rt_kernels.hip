@@ -39,6 +39,7 @@ thread_local std::string g_error;
 void set_error(const std::string& s) { g_error = s; }
 uint32_t g_profiling = 0;       // stage mask: bit k = rt_kernel_stage k timed with HIP events
 uint32_t g_pool_override = 0;
+int g_splat_mode = RT_SPLAT_STREAM;
 }
 
 // Tables embedded from data/ (extracted from the reference by tools/extract_tables.py).
@@ -1111,6 +1112,13 @@ struct Pool {
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
     uint32_t* free_n;    // [blocks]: slots per BLOCK-slot block free for the next k_generate (k_shade)
     uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
+    // This partition's sample records (the deterministic splats): pass s, tile-list pixel p at
+    // ((s - rec_pass0) % rec_ring)*P + p.  A ring of rec_ring passes in the streaming splat
+    // (k_resolve_tiles frees passes while the frame renders), the partition's whole pass range
+    // in the exact splat (k_resolve).  Null: atomic splat.
+    float4*  rec_rgbx;   // r, g, b, jitter_x
+    float*   rec_jy;     // jitter_y
+    uint32_t rec_pass0, rec_ring;
 };
 
 // Slot states.  Every per-iteration kernel except the tracers walks the pool in
@@ -1144,6 +1152,13 @@ struct Counters {
     unsigned long long closest_rays;
     unsigned long long shadow_rays;
     unsigned long long traced_rays[2];   // handed to k_trace<false> / k_trace<true>
+    // streaming splat (k_bookkeep plans, k_resolve_tiles consumes)
+    unsigned long long claim_limit;      // samples below this may be claimed: the record ring's capacity
+    unsigned long long start_sample;     // the partition's first sample
+    uint32_t iter;                       // iterations bookkept so far
+    uint32_t res_cursor;                 // passes below it are resolved (or planned for the next resolve)
+    uint32_t res_from, res_to;           // the pass range the next k_resolve_tiles resolves (empty: none)
+    unsigned long long hist[128];        // next_sample after the bookkeep of iteration i, at [i % 128]
 };
 
 struct FrameParams {
@@ -1283,7 +1298,12 @@ RT_D void block_tally(const bool (&pred)[K], uint32_t* const (&ctr)[K], uint32_t
     }
 }
 
-RT_D unsigned long long remaining_samples(const Counters* c) { return c->total_samples - c->next_sample; }
+// Samples still to be claimed now: up to the partition's end, and (streaming splat) no further than
+// the record ring holds.
+RT_D unsigned long long remaining_samples(const Counters* c) {
+    const unsigned long long lim = c->claim_limit < c->total_samples ? c->claim_limit : c->total_samples;
+    return lim > c->next_sample ? lim - c->next_sample : 0ull;
+}
 
 // ---- lens (RT/raytracer.cpp:86-123)
 RT_D V2 transform_bokeh_sample(V2 o, float f, float n, float phi_shutter_max) {
@@ -1352,15 +1372,17 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
             const uint32_t k = __float_as_uint(pool.ray_d[slot].w);
             float* o = fp.list_out + 5*(size_t)k;
             o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = j.x; o[4] = j.y;
-        } else if (fp.samp_rgbx) {
-            // deterministic path: store the sample; k_resolve gathers it in reference order
-            const size_t rec = (size_t)__float_as_uint(pool.ray_d[slot].w)*fp.pixels + __float_as_uint(pool.prev_n[slot].w);
+        } else if (pool.rec_rgbx) {
+            // deterministic paths: store the sample; k_resolve_tiles / k_resolve gather it
+            const uint32_t rel = __float_as_uint(pool.ray_d[slot].w) - pool.rec_pass0;
+            const size_t rec = (size_t)(rel < pool.rec_ring ? rel : rel % pool.rec_ring)*fp.pixels +
+                               __float_as_uint(pool.prev_n[slot].w);
 #if RT_NT_SPLAT
-            stnt(&fp.samp_rgbx[rec], make_float4(r.x, r.y, r.z, j.x));      // read again only by k_resolve
-            stnt(&fp.samp_jy[rec], j.y);
+            stnt(&pool.rec_rgbx[rec], make_float4(r.x, r.y, r.z, j.x));     // read again only by the resolve
+            stnt(&pool.rec_jy[rec], j.y);
 #else
-            fp.samp_rgbx[rec] = make_float4(r.x, r.y, r.z, j.x);
-            fp.samp_jy[rec] = j.y;
+            pool.rec_rgbx[rec] = make_float4(r.x, r.y, r.z, j.x);
+            pool.rec_jy[rec] = j.y;
 #endif
         } else if (fp.cache_size) {
             const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
@@ -1409,6 +1431,14 @@ __global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out
         out[base + local] = (min_x + local % tw) | ((min_y + local / tw) << 16);
 }
 
+// k_generate reads only the sampler tables and the ray prologue's tables, which stay in HBM
+// (RT_LDS_STRATA = 0) and are read through the scalar cache (RT_PROLOGUE_SCALAR): a block
+// needs no LDS copy of the scene, so it skips that copy, its barrier and its LDS footprint.
+#ifndef RT_GEN_LDS_SCENE
+#define RT_GEN_LDS_SCENE (!RT_PROLOGUE_SCALAR || RT_LDS_STRATA)
+#endif
+constexpr uint32_t GEN_LDS_Q_SCALE = RT_GEN_LDS_SCENE ? 16u : 0u;   // dynamic LDS bytes per blob float4
+
 // k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
 __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                     Counters* cnt, int cur) {
@@ -1426,7 +1456,11 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     }
     // No sample left for this block to claim (the frame's drain): splat only, no scene copy
     if ((unsigned long long)pool.claim_base[blockIdx.x] >= remaining_samples(cnt)) return;
+#if RT_GEN_LDS_SCENE
     const DevScene sc = scene_in_lds(sc_g, lds_scene);
+#else
+    const DevScene& sc = sc_g;       // nothing generate reads lives in the LDS copy (see RT_GEN_LDS_SCENE)
+#endif
     const bool own_free = own_state != S_TRACE;
     uint32_t nfree;
     const uint32_t rank = block_rank<BLOCK>(own_free, agg, &nfree);
@@ -2086,17 +2120,189 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
         if (Y0 + r < H) fp.accum[(size_t)(Y0 + r)*W + X] = acc[r];
 }
 
+// k_resolve_tiles — splat_filter (RT/raytracer.cpp:187-259, :476-488) as a gather that
+// reads every sample record from HBM once (the streaming splat, the default).
+//
+// A workgroup owns a 64 x 16 block of output pixels; a thread owns a column strip of
+// TR_ROWS of them, accumulated in registers.  Per sample pass s of the planned range
+// [res_from, res_to) the workgroup stages the records of the block's source region (the
+// block plus the filter radius on every side, from the owned tiles only) into LDS with
+// one coalesced load each, and every thread sums its strip's (2r+1)^2 windows out of LDS.
+// The next pass's records are loaded into registers while the current one is summed.
+//
+// Per output pixel the sum runs pass by pass, and inside a pass over the window rows and
+// columns in ascending order, from the value the buffer held: deterministic, and the same
+// however the passes are split between launches (an f32 load and store in between changes
+// nothing).  It is not the reference's order (tiles descending, pixels, then samples,
+// k_resolve), so it matches the reference's frame to float rounding, not bit for bit; the
+// filter weight is the reference's LUT product fx*fy, accumulated with an FMA.  The box
+// filter (cache_size 0) adds (L, 1) to the pixel's own sum in sample order, which IS the
+// reference's order.
+//
+// Partition k resolves its own pass range into its own buffer (the caller's for k = 0),
+// so partitions never write the same buffer; k_combine_partials adds them up at the end.
+constexpr int TR_W = 64, TR_H = 16, TR_THREADS = 256, TR_ROWS = TR_H / (TR_THREADS / TR_W);
+__host__ __device__ constexpr int tr_stage_slots(int ks) { return ((TR_W + 2*ks)*(TR_H + 2*ks) + TR_THREADS - 1) / TR_THREADS; }
+__host__ __device__ constexpr size_t tr_lds_bytes(int ks) {
+    return (size_t)(TR_W + 2*ks)*(TR_H + 2*ks)*(16 + 4) + 512*4;
+}
+template <int KSMAX>
+__global__ void __launch_bounds__(TR_THREADS) k_resolve_tiles(FrameParams fp, Pool pool, const Counters* cnt,
+                                                               const uint32_t* blocks, float4* dst) {
+    const uint32_t s0 = cnt->res_from, s1 = cnt->res_to;
+    if (s0 >= s1) return;
+    constexpr int NST = tr_stage_slots(KSMAX);
+    extern __shared__ float4 tr_lds[];
+    const int ks = fp.cache_size ? fp.kernel_size : 0;
+    const int SW = TR_W + 2*ks, SH = TR_H + 2*ks, N = SW*SH;
+    float4* srgb = tr_lds;                                          // [N] r, g, b, jitter_x
+    float* sjy = reinterpret_cast<float*>(tr_lds + N);              // [N] jitter_y (NaN: not an owned sample)
+    float* lut = sjy + N;                                           // [512]
+    const int tid = threadIdx.x;
+    const int W = (int)fp.w, H = (int)fp.h;
+    const uint32_t blk = blocks[blockIdx.x];
+    const int x0 = (int)(blk & 0xFFFFu)*TR_W, y0 = (int)(blk >> 16)*TR_H;
+    const int xs0 = x0 - ks, ys0 = y0 - ks;
+    for (int i = tid; i < 512; i += TR_THREADS) lut[i] = fp.cache_size ? fp.lut[i] : 0.0f;
+    // the tile-list pixel of each staged source pixel (kept in registers for the stage loads)
+    int myp[NST];
+#pragma unroll
+    for (int k = 0; k < NST; ++k) {
+        const int i = tid + k*TR_THREADS;
+        int pi = -1;
+        const int sx = xs0 + i % SW, sy = ys0 + i / SW;
+        if (i < N && sx >= 0 && sx < W && sy >= 0 && sy < H) {
+            const int tx = sx / (int)fp.tile_w, ty = sy / (int)fp.tile_h;
+            const int base = fp.tile_base[ty*(int)fp.tcx + tx];
+            if (base >= 0) {
+                const int min_x = tx*(int)fp.tile_w, min_y = ty*(int)fp.tile_h;
+                const int twid = min(W, min_x + (int)fp.tile_w) - min_x;
+                pi = base + (sy - min_y)*twid + (sx - min_x);
+            }
+        }
+        myp[k] = pi;
+    }
+    const size_t P = fp.pixels;
+    float4 pc[NST];
+    float pj[NST];
+    auto load_pass = [&](uint32_t s) {
+        const uint32_t rel = s - pool.rec_pass0;
+        const size_t base = (size_t)(rel < pool.rec_ring ? rel : rel % pool.rec_ring)*P;
+#pragma unroll
+        for (int k = 0; k < NST; ++k) {
+            if (myp[k] >= 0) {
+                pc[k] = ldnt(&pool.rec_rgbx[base + (size_t)myp[k]]);
+                pj[k] = ldnt(&pool.rec_jy[base + (size_t)myp[k]]);
+            } else {
+                pc[k] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+                pj[k] = __builtin_nanf("");
+            }
+        }
+    };
+    // this thread's output strip: column X, rows Y0 .. Y0 + TR_ROWS - 1
+    const int X = x0 + tid % TR_W, Y0 = y0 + (tid / TR_W)*TR_ROWS;
+    const bool col_in = X < W;
+    float4 acc[TR_ROWS];
+#pragma unroll
+    for (int r = 0; r < TR_ROWS; ++r)
+        acc[r] = (col_in && Y0 + r < H) ? dst[(size_t)(Y0 + r)*W + X] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const bool box = !fp.cache_size;
+    const float kscale = ks ? (float)(fp.cache_size - 1) / (float)ks : 0.0f;
+    const int xa = max(X - ks, 0), xb = min(X + ks, W - 1);
+    const int ya = max(Y0 - ks, 0), yb = min(Y0 + TR_ROWS - 1 + ks, H - 1);
+    load_pass(s0);
+    for (uint32_t s = s0; s < s1; ++s) {
+        __syncthreads();                                    // the previous pass's sums are done with LDS
+#pragma unroll
+        for (int k = 0; k < NST; ++k) {
+            const int i = tid + k*TR_THREADS;
+            if (i < N) { srgb[i] = pc[k]; sjy[i] = pj[k]; }
+        }
+        __syncthreads();
+        if (s + 1 < s1) load_pass(s + 1);                   // in flight while this pass is summed
+        if (!col_in) continue;
+        for (int sy = ya; sy <= yb; ++sy) {
+            const int rlo = max(sy - ks - Y0, 0), rhi = min(sy + ks - Y0, TR_ROWS - 1);
+            const int row = (sy - ys0)*SW - xs0;
+            for (int sx = xa; sx <= xb; ++sx) {
+                const float jy = sjy[row + sx];
+                if (jy != jy) continue;                     // not a sample of this shard
+                const float4 c = srgb[row + sx];
+                if (box) {                                  // (result, 1) into the pixel itself
+#pragma unroll
+                    for (int r = 0; r < TR_ROWS; ++r)
+                        if (r == sy - Y0) {
+                            acc[r].x = acc[r].x + c.x; acc[r].y = acc[r].y + c.y;
+                            acc[r].z = acc[r].z + c.z; acc[r].w = acc[r].w + 1.0f;
+                        }
+                    continue;
+                }
+                const float fx = lut[(int)fabsf(0.5f + kscale*((float)(X - sx) - c.w))];
+#pragma unroll
+                for (int r = 0; r < TR_ROWS; ++r) {
+                    if (r < rlo || r > rhi) continue;
+                    const float fy = lut[(int)fabsf(0.5f + kscale*((float)(Y0 + r - sy) - jy))];
+                    const float f = fx*fy;
+                    acc[r].x = fmaf(f, c.x, acc[r].x);
+                    acc[r].y = fmaf(f, c.y, acc[r].y);
+                    acc[r].z = fmaf(f, c.z, acc[r].z);
+                    acc[r].w = acc[r].w + f;
+                }
+            }
+        }
+    }
+    if (col_in) {
+#pragma unroll
+        for (int r = 0; r < TR_ROWS; ++r)
+            if (Y0 + r < H) dst[(size_t)(Y0 + r)*W + X] = acc[r];
+    }
+}
+
+// The partitions' buffers added to the caller's, in partition order (streaming splat).
+__global__ void __launch_bounds__(256) k_combine_partials(float4* accum, const float4* const* parts, int nparts, size_t n) {
+    for (size_t i = (size_t)blockIdx.x*256 + threadIdx.x; i < n; i += (size_t)gridDim.x*256) {
+        float4 a = accum[i];
+        for (int k = 0; k < nparts; ++k) {
+            const float4 b = ldnt(&parts[k][i]);
+            a.x = a.x + b.x; a.y = a.y + b.y; a.z = a.z + b.z; a.w = a.w + b.w;
+        }
+        accum[i] = a;
+    }
+}
+
 // k_bookkeep — end of iteration (one workgroup): ray counts, counter roll-over,
 // and the exclusive scan of the per-block free counts that gives every block of
-// the next k_generate its first sample claim.  `first` = before the first
-// iteration (only the scan).
+// the next k_generate its first sample claim.  Phase BK_FIRST = before the first
+// iteration (only the scan); BK_FINAL = after the partition's last iteration (only
+// the resolve plan).
+//
+// Streaming splat: a path claimed by the k_generate of iteration j has made its last
+// bounce by the k_shade of iteration j + max(max_bounce_count, 1) - 1 (one bounce per
+// iteration), and its sample record is written by the next k_generate.  So once
+// iteration i is bookkept, every sample claimed up to iteration i - life is in the
+// record ring (life = max(max_bounce_count, 1)): hist[] holds the claim cursor per
+// iteration.  With plan.mode set (the host launches k_resolve_tiles right after this
+// kernel), the passes complete since the last plan become the next resolve's range
+// once there are plan.chunk of them (or all that remain, BK_FINAL), and the claim
+// limit moves to keep the ring from overwriting passes not yet resolved.
+enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
+struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life; };
 constexpr int BK_THREADS = 1024;
-__global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int first) {
+__global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
+                                                         ResPlan plan) {
     __shared__ uint32_t sc[BK_THREADS];
     __shared__ uint32_t carry;
     const uint32_t t = threadIdx.x;
+    if (phase == BK_FINAL) {
+        if (t == 0) {
+            cnt->res_from = cnt->res_cursor;
+            cnt->res_to = plan.pass1;
+            cnt->res_cursor = plan.pass1;
+        }
+        return;
+    }
     if (t == 0) {
-        if (!first) {
+        if (phase == BK_ITER) {
             const unsigned long long rem = remaining_samples(cnt);
             cnt->next_sample += ((unsigned long long)cnt->gen_free < rem ? (unsigned long long)cnt->gen_free : rem);
             uint32_t ext = 0, sh = 0, pend = 0, tq = 0, ts = 0, ps = 0;
@@ -2122,6 +2328,21 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             cnt->traced_rays[1] += ts;
             cnt->pending = pend;
             cnt->pending_splat = ps;
+            const uint32_t it = cnt->iter++;
+            cnt->hist[it & 127u] = cnt->next_sample;
+            if (plan.mode) {
+                const unsigned long long done = it >= plan.life ? cnt->hist[(it - plan.life) & 127u] : cnt->start_sample;
+                const uint32_t done_pass = (uint32_t)(done / plan.P);
+                const uint32_t from = cnt->res_cursor;
+                cnt->res_from = cnt->res_to = 0;
+                if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
+                    cnt->res_from = from;
+                    cnt->res_to = done_pass;
+                    cnt->res_cursor = done_pass;
+                    // the ring slots of [from, done_pass) are free once the resolve launched next has run
+                    cnt->claim_limit = (unsigned long long)(done_pass + plan.ring)*plan.P;
+                }
+            }
         }
         carry = 0;
     }
@@ -2276,6 +2497,7 @@ struct Partition {
     hipStream_t own_stream = nullptr;   // partitions > 0 (partition 0 runs on the caller's stream)
     hipEvent_t join = nullptr;
     hipEvent_t ev[EV_SLOTS * 2 * RT_KERNEL_COUNT] = {};
+    hipEvent_t ev_final[2] = {};        // the partition's last k_resolve_tiles (streaming splat)
     bool events = false;
 };
 
@@ -2297,6 +2519,10 @@ struct rt_scene {
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
     float* d_lut = nullptr;
+    float4* d_partials = nullptr;   // streaming splat: partitions 1.. accumulate here
+    size_t partial_cap = 0;
+    uint32_t* d_aux = nullptr;      // streaming splat: partial pointers, then k_resolve_tiles' blocks
+    size_t aux_cap = 0;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
 };
@@ -2451,7 +2677,10 @@ void free_partition(Partition& pt) {
     if (pt.own_stream) (void)hipStreamDestroy(pt.own_stream);
     if (pt.join) (void)hipEventDestroy(pt.join);
     for (auto& e : pt.chunk_done) if (e) (void)hipEventDestroy(e);
-    if (pt.events) for (auto& e : pt.ev) (void)hipEventDestroy(e);
+    if (pt.events) {
+        for (auto& e : pt.ev) (void)hipEventDestroy(e);
+        for (auto& e : pt.ev_final) (void)hipEventDestroy(e);
+    }
     pt = Partition{};
 }
 
@@ -2516,40 +2745,84 @@ int check_inputs(const rt_settings* st, const rt_filter_cache* f) {
     return RT_OK;
 }
 
-// The wavefront driver shared by rt_render_device and rt_trace_samples.
-// The frame's samples [0, total) are split into contiguous ranges, one per
-// partition (RT_PARTITIONS, default 4); each partition runs generate -> extend ->
-// shade -> connect -> splat -> bookkeep on its own stream, and the host enqueues
-// the partitions' iterations interleaved.  Results do not depend on the split:
-// every sample is keyed by its own number (the RNG seed and the record slot).
-int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long long total, hipStream_t stream, rt_stats* stats) {
-    auto t0 = std::chrono::steady_clock::now();
-    int nparts = 4;
-    if (const char* e = getenv("RT_PARTITIONS")) nparts = std::max(1, std::min(MAX_PARTITIONS, atoi(e)));
-    // Paths per partition: a larger pool amortizes each trace launch's tail (its slowest
-    // ray) over more rays, until the pool is so large that the frame is only a few pool
-    // fills and the final drain dominates.  An eighth of the partition's samples, between
-    // 2^21 and 3 x 2^21 (~3 GB of path state and queues).  C3 256 spp on one box: 1M 6552,
-    // 2M 8128, 4M 8613 / 8895, 6M 9058, 8M 9054 Mrays/s; rank 0 of 8 (16.6M samples per
-    // partition): 1M 60.4, 2M 51.0, 4M 51.2, 6M 55.3 ms
+// Partitions and path pool of a frame of `total` samples (`passes` sample passes over the
+// shard's pixels; 0 = an explicit sample list).  A larger pool amortizes each trace
+// launch's tail (its slowest ray) over more rays, until the pool is so large that the
+// frame is only a few pool fills and the final drain dominates: an eighth of the
+// partition's samples, between 2^21 and 3 x 2^21 (~3 GB of path state and queues).  C3
+// 256 spp on one box: 1M 6552, 2M 8128, 4M 8613 / 8895, 6M 9058, 8M 9054 Mrays/s; rank 0
+// of 8 (16.6M samples per partition): 1M 60.4, 2M 51.0, 4M 51.2, 6M 55.3 ms.
+struct FrameShape { int nparts; uint32_t pool_n; };
+FrameShape frame_shape(unsigned long long total, uint32_t passes) {
+    FrameShape f;
+    f.nparts = 4;
+    if (const char* e = getenv("RT_PARTITIONS")) f.nparts = std::max(1, std::min(MAX_PARTITIONS, atoi(e)));
+    if (passes) f.nparts = std::max(1, std::min<int>(f.nparts, (int)passes));   // partitions own whole passes
     uint32_t pool_n = g_pool_override;
     if (!pool_n) {
-        const unsigned long long want = total / (unsigned long long)nparts / 8ull;
+        const unsigned long long want = total / (unsigned long long)f.nparts / 8ull;
         pool_n = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>(want, 1ull << 21), 3ull << 21);
     }
     // small frames: one partition, pool no larger than the work
-    if ((unsigned long long)pool_n*nparts > total) nparts = 1;
+    if ((unsigned long long)pool_n*f.nparts > total) f.nparts = 1;
     if ((unsigned long long)pool_n > total) pool_n = (uint32_t)std::max<unsigned long long>(total, 1ull);
-    pool_n = (pool_n + BLOCK - 1) / BLOCK * BLOCK;
+    f.pool_n = (pool_n + BLOCK - 1) / BLOCK * BLOCK;
+    return f;
+}
+
+// How a frame's samples reach the accumulation buffer (rt_set_splat_mode).
+struct SplatCfg {
+    int mode = RT_SPLAT_ATOMIC;         // rt_splat_mode; ATOMIC also for explicit sample lists
+    uint32_t passes = 0;                // samples per pixel of the frame
+    uint32_t ring = 0, chunk = 0;       // STREAM: record-ring passes per partition, passes per resolve
+    float4* rec = nullptr;              // STREAM: nparts rings of ring*P; EXACT: spp*P, pass-major
+    float* rec_jy = nullptr;
+    const uint32_t* blocks = nullptr;   // STREAM: k_resolve_tiles' output blocks
+    uint32_t nblocks = 0;
+    int ksmax = 2;                      // STREAM: k_resolve_tiles instantiation
+    size_t lds = 0;
+    float4* partials = nullptr;         // STREAM: partitions 1.. accumulate here (w*h each)
+    const float4* const* part_ptrs = nullptr;   // device array of the partials' addresses
+};
+
+void launch_resolve_tiles(const SplatCfg& sp, const FrameParams& fp, const Pool& pool, const Counters* cnt,
+                          float4* dst, hipStream_t q) {
+    switch (sp.ksmax) {
+        case 2:  k_resolve_tiles<2><<<sp.nblocks, TR_THREADS, sp.lds, q>>>(fp, pool, cnt, sp.blocks, dst); break;
+        case 4:  k_resolve_tiles<4><<<sp.nblocks, TR_THREADS, sp.lds, q>>>(fp, pool, cnt, sp.blocks, dst); break;
+        default: k_resolve_tiles<12><<<sp.nblocks, TR_THREADS, sp.lds, q>>>(fp, pool, cnt, sp.blocks, dst); break;
+    }
+}
+
+// The wavefront driver shared by rt_render_device and rt_trace_samples.
+// The frame's samples [0, total) are split into contiguous ranges, one per
+// partition (RT_PARTITIONS, default 4; whole sample passes each when the frame is
+// rendered); each partition runs generate -> extend -> shade -> connect -> bookkeep
+// on its own stream, and the host enqueues the partitions' iterations interleaved.
+// Every sample is keyed by its own number (the RNG seed and the record slot), so the
+// samples do not depend on the split.  The streaming splat resolves each partition's
+// passes into its own buffer while the frame renders (k_resolve_tiles after the
+// bookkeep of every chunk's last iteration), and the buffers are added at the end.
+int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long long total, hipStream_t stream,
+              const SplatCfg& sp, rt_stats* stats) {
+    auto t0 = std::chrono::steady_clock::now();
+    const bool listed = fp.list_xy != nullptr;
+    const FrameShape shape = frame_shape(total, listed ? 0u : sp.passes);
+    const int nparts = shape.nparts;
+    const uint32_t pool_n = shape.pool_n;
+    const bool stream_splat = !listed && sp.mode == RT_SPLAT_STREAM;
+    const size_t npx = (size_t)fp.w*fp.h;
     const uint32_t prof = g_profiling & ~(1u << RT_KERNEL_SPLAT);   // the splat runs inside k_generate
     const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(s->start_ev, stream));
     struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live; int final_buf;
-                 uint64_t chunk_first[2]; int chunk_n[2]; };
+                 uint64_t chunk_first[2]; int chunk_n[2]; uint32_t pass0, pass1, ring; float4* dst;
+                 bool res_ev[EV_SLOTS]; };
     Run run[MAX_PARTITIONS] = {};
     double kms[RT_KERNEL_COUNT] = {};
     uint64_t klaunch[RT_KERNEL_COUNT] = {};
+    const uint32_t life = std::max<uint32_t>(st->max_bounce_count, 1u);
     for (int k = 0; k < nparts; ++k) {
         int err = ensure_partition(s, k);
         if (!err) err = ensure_pool(s->part[k], pool_n);
@@ -2562,17 +2835,48 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         r.grid = (N + BLOCK - 1) / BLOCK;
         r.live = true;
         Counters init = {};
-        init.next_sample = total*(unsigned long long)k / nparts;
-        init.total_samples = total*(unsigned long long)(k + 1) / nparts;
+        init.claim_limit = ~0ull;
+        Pool& pool = pt.pool;
+        pool.rec_rgbx = nullptr; pool.rec_jy = nullptr; pool.rec_pass0 = 0; pool.rec_ring = 1;
+        if (listed) {
+            init.next_sample = total*(unsigned long long)k / nparts;
+            init.total_samples = total*(unsigned long long)(k + 1) / nparts;
+        } else {
+            r.pass0 = (uint32_t)((unsigned long long)sp.passes*k / nparts);
+            r.pass1 = (uint32_t)((unsigned long long)sp.passes*(k + 1) / nparts);
+            init.next_sample = (unsigned long long)r.pass0*fp.pixels;
+            init.total_samples = (unsigned long long)r.pass1*fp.pixels;
+            init.res_cursor = r.pass0;
+            pool.rec_pass0 = r.pass0;
+            if (sp.mode == RT_SPLAT_EXACT) {                   // the global pass-major layout, s*P + p
+                pool.rec_rgbx = sp.rec + (size_t)r.pass0*fp.pixels;
+                pool.rec_jy = sp.rec_jy + (size_t)r.pass0*fp.pixels;
+                pool.rec_ring = std::max(1u, r.pass1 - r.pass0);
+            } else if (stream_splat) {
+                r.ring = std::min(sp.ring, std::max(1u, r.pass1 - r.pass0));
+                pool.rec_rgbx = sp.rec + (size_t)k*sp.ring*fp.pixels;
+                pool.rec_jy = sp.rec_jy + (size_t)k*sp.ring*fp.pixels;
+                pool.rec_ring = r.ring;
+                init.claim_limit = (unsigned long long)(r.pass0 + r.ring)*fp.pixels;
+                r.dst = k ? sp.partials + (size_t)(k - 1)*npx : fp.accum;
+                if (k) HIP_OK(hipMemsetAsync(r.dst, 0, sizeof(float4)*npx, r.stream));
+            }
+        }
+        init.start_sample = init.next_sample;
         HIP_OK(hipMemcpyAsync(pt.cnt, &init, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
-        k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, 0, 1);
+        k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{});
         if (prof && !pt.events) {
             for (auto& e : pt.ev) HIP_OK(hipEventCreate(&e));
+            for (auto& e : pt.ev_final) HIP_OK(hipEventCreate(&e));
             pt.events = true;
         }
     }
+    auto plan_of = [&](int k, uint32_t mode) {
+        const Run& r = run[k];
+        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, life};
+    };
     // Stage timing without extra host syncs: each iteration records begin/end
     // events into one of EV_SLOTS ring slots; a chunk's slots are read back when
     // the host has waited for that chunk anyway.
@@ -2584,8 +2888,9 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if (!prof) return;
         for (int i = 0; i < r.chunk_n[b]; ++i) {
             const int slot = (int)((r.chunk_first[b] + i) % EV_SLOTS);
-            for (int kern = 0; kern < RT_KERNEL_COUNT - 1; ++kern) {
-                if (!((prof >> kern) & 1u)) continue;
+            for (int kern = 0; kern < RT_KERNEL_COUNT; ++kern) {
+                if (!((prof >> kern) & 1u) || kern == RT_KERNEL_SPLAT) continue;
+                if (kern == RT_KERNEL_RESOLVE && !r.res_ev[slot]) continue;
                 float ms = 0.0f;
                 if (hipEventElapsedTime(&ms, ev(k, slot, kern, 0), ev(k, slot, kern, 1)) == hipSuccess) {
                     kms[kern] += ms; klaunch[kern] += 1;
@@ -2593,7 +2898,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             }
         }
     };
-    auto iterate = [&](int k) {
+    auto iterate = [&](int k, bool plan) {
         Partition& pt = s->part[k];
         Run& r = run[k];
         const hipStream_t q = r.stream;
@@ -2601,7 +2906,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         auto b = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
         auto e = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
         b(RT_KERNEL_GENERATE);
-        k_generate<<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        k_generate<<<r.grid, BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
         if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
@@ -2611,7 +2916,14 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_CONNECT);
-        k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pt.pool, r.grid, r.cur, 0);
+        const bool res = stream_splat && plan;
+        k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pt.pool, r.grid, r.cur, BK_ITER, plan_of(k, res ? 1u : 0u));
+        r.res_ev[slot] = res && ((prof >> RT_KERNEL_RESOLVE) & 1u);
+        if (res) {                       // the passes the bookkeep found complete, if enough of them
+            b(RT_KERNEL_RESOLVE);
+            launch_resolve_tiles(sp, fp, pt.pool, pt.cnt, r.dst, q);
+            e(RT_KERNEL_RESOLVE);
+        }
         ++r.iters;
         r.cur ^= 1;
     };
@@ -2625,11 +2937,24 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         const int b = (int)(r.chunks & 1);
         r.chunk_first[b] = r.iters;
         r.chunk_n[b] = r.chunks < 3 ? 1 : 4;
-        for (int i = 0; i < r.chunk_n[b]; ++i) iterate(k);
+        for (int i = 0; i < r.chunk_n[b]; ++i) iterate(k, i == r.chunk_n[b] - 1);
         HIP_OK(hipGetLastError());
         HIP_OK(hipMemcpyAsync(pt.cnt_host + b, pt.cnt, sizeof(Counters), hipMemcpyDeviceToHost, r.stream));
         HIP_OK(hipEventRecord(pt.chunk_done[b], r.stream));
         ++r.chunks;
+        return RT_OK;
+    };
+    // A partition whose samples are all splatted resolves whatever passes are left.
+    auto finish = [&](int k) -> int {
+        if (!stream_splat) return RT_OK;
+        Partition& pt = s->part[k];
+        Run& r = run[k];
+        k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, r.cur, BK_FINAL, plan_of(k, 2u));
+        const bool t = (prof >> RT_KERNEL_RESOLVE) & 1u;
+        if (t) HIP_OK(hipEventRecord(pt.ev_final[0], r.stream));
+        launch_resolve_tiles(sp, fp, pt.pool, pt.cnt, r.dst, r.stream);
+        if (t) HIP_OK(hipEventRecord(pt.ev_final[1], r.stream));
+        HIP_OK(hipGetLastError());
         return RT_OK;
     };
     s->cancel = 0;
@@ -2650,17 +2975,40 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             const Counters& c = s->part[k].cnt_host[b];
             if (c.next_sample >= c.total_samples && c.pending == 0 && c.pending_splat == 0) {
                 r.live = false; r.final_buf = b; --live;       // its chunk still in flight finds nothing to do
+                int err = finish(k);
+                if (err) return err;
             } else {
                 int err = enqueue_chunk(k);
                 if (err) return err;
             }
         }
-        if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
-        if (rounds > 100000) { set_error("wavefront loop did not converge"); return RT_ERROR_DEVICE; }
+        if (s->cancel || rounds > 1000000) {
+            // Every partition may still have two chunks in flight that write the pool, the sample
+            // records or (atomic splat) the caller's accumulation buffer: wait for them before the
+            // error returns, so the caller may reuse its memory at once.
+            for (int k = 0; k < nparts; ++k) (void)hipStreamSynchronize(run[k].stream);
+            if (s->cancel) { set_error("render cancelled"); return RT_ERROR_CANCELLED; }
+            set_error("wavefront loop did not converge");
+            return RT_ERROR_DEVICE;
+        }
     }
     for (int k = 1; k < nparts; ++k) {                     // the caller's stream continues after every partition
         HIP_OK(hipEventRecord(s->part[k].join, run[k].stream));
         HIP_OK(hipStreamWaitEvent(stream, s->part[k].join, 0));
+    }
+    if (stream_splat && nparts > 1) {
+        k_combine_partials<<<(uint32_t)std::min<size_t>((npx + 255) / 256, 8192), 256, 0, stream>>>(
+            fp.accum, sp.part_ptrs, nparts - 1, npx);
+        HIP_OK(hipGetLastError());
+    }
+    if (stream_splat && ((prof >> RT_KERNEL_RESOLVE) & 1u)) {
+        HIP_OK(hipStreamSynchronize(stream));
+        for (int k = 0; k < nparts; ++k) {
+            float ms = 0.0f;
+            if (hipEventElapsedTime(&ms, s->part[k].ev_final[0], s->part[k].ev_final[1]) == hipSuccess) {
+                kms[RT_KERNEL_RESOLVE] += ms; klaunch[RT_KERNEL_RESOLVE] += 1;
+            }
+        }
     }
     Counters sum = {};
     uint64_t iters = 0;
@@ -2745,6 +3093,11 @@ int rt_device_count(int* out) {
 int rt_set_profiling(int enable) { g_profiling = enable ? (1u << RT_KERNEL_COUNT) - 1u : 0u; return RT_OK; }
 int rt_set_profiling_stages(uint32_t mask) { g_profiling = mask & ((1u << RT_KERNEL_COUNT) - 1u); return RT_OK; }
 int rt_set_path_pool(uint32_t paths) { g_pool_override = paths; return RT_OK; }
+int rt_set_splat_mode(int mode) {
+    if (mode < RT_SPLAT_STREAM || mode > RT_SPLAT_ATOMIC) { set_error("bad splat mode"); return RT_ERROR_INVALID; }
+    g_splat_mode = mode;
+    return RT_OK;
+}
 
 int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     if (!d || !out) { set_error("null argument"); return RT_ERROR_INVALID; }
@@ -3019,6 +3372,8 @@ int rt_scene_free(rt_scene* s) {
     if (s->d_samp) (void)hipFree(s->d_samp);
     if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
     if (s->d_lut) (void)hipFree(s->d_lut);
+    if (s->d_partials) (void)hipFree(s->d_partials);
+    if (s->d_aux) (void)hipFree(s->d_aux);
     delete s;
     return RT_OK;
 }
@@ -3089,12 +3444,14 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     uint32_t tcy = (h + tiles->tile_h - 1) / tiles->tile_h;
     // owned tiles: t % shard_count == shard_index, descending like the reference's queue (:555)
     std::vector<uint32_t> ids, prefix(1, 0);
+    uint64_t owned_px = 0;
     for (uint32_t t = fp.tcx*tcy; t-- > 0;) {
         if (t % tiles->shard_count != tiles->shard_index) continue;
         uint32_t min_x = tiles->tile_w*(t % fp.tcx), min_y = tiles->tile_h*(t / fp.tcx);
         uint32_t tw = std::min(w, min_x + tiles->tile_w) - min_x, th = std::min(h, min_y + tiles->tile_h) - min_y;
         ids.push_back(t);
-        prefix.push_back(prefix.back() + tw*th);
+        owned_px += (uint64_t)tw*th;
+        prefix.push_back((uint32_t)std::min<uint64_t>(owned_px, 0xFFFFFFFFull));
     }
     if (ids.empty()) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
     size_t need = ids.size() + prefix.size();
@@ -3111,8 +3468,11 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.ntiles = (uint32_t)ids.size();
     fp.tile_ids = s->d_tiles;
     fp.tile_prefix = s->d_tiles + ids.size();
-    fp.pixels = prefix.back();
     if (w > 65535 || h > 65535) { set_error("frame larger than 65535 pixels a side"); return RT_ERROR_INVALID; }
+    if (owned_px >= 0x80000000ull) {        // tile_base / pixel indices are 31-bit
+        set_error("shard of 2^31 or more pixels: use more shards"); return RT_ERROR_INVALID;
+    }
+    fp.pixels = prefix.back();
     if (s->pixmap_cap < fp.pixels) {
         if (s->d_pixmap) (void)hipFree(s->d_pixmap);
         s->d_pixmap = nullptr; s->pixmap_cap = 0;
@@ -3129,9 +3489,15 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.accum = reinterpret_cast<float4*>(d_pixels);
     unsigned long long total = (unsigned long long)fp.pixels*st->samples_per_pixel;
     if (total == 0) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
-    // Deterministic splat (k_resolve) needs spp*P 20-byte sample records in HBM.  The
-    // budget is the device's free memory (plus the records already held) less 16 GB for
-    // the partitions' path pools; above it the frame falls back to float-atomic splats.
+    // The splat (rt_set_splat_mode).  Both deterministic modes keep a 20-byte record per
+    // sample in HBM: STREAM a ring of `ring` passes per partition (k_resolve_tiles frees
+    // passes as the frame renders), EXACT the whole frame (k_resolve at the end, the
+    // reference's order).  The budget is the free memory (plus the records already held)
+    // less 16 GB for the partitions' path pools.  EXACT falls back to STREAM over budget or
+    // past the filter radius k_resolve_tiles stages (12); STREAM to ATOMIC only if even
+    // one pass per partition does not fit.
+    const uint32_t spp = st->samples_per_pixel;
+    const int ks = fp.cache_size ? fp.kernel_size : 0;
     double budget;
     if (const char* bud = getenv("RT_SAMPLE_BUDGET_GB")) {
         budget = atof(bud)*1e9;
@@ -3140,22 +3506,47 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
         budget = (double)free_b + 20.0*(double)s->samp_cap - 16e9;
     }
-    bool gather = (double)total*20.0 <= budget;
-    if (gather && s->samp_cap < total) {
+    SplatCfg sp;
+    sp.passes = spp;
+    sp.mode = g_splat_mode;
+    if (const char* e = getenv("RT_SPLAT")) sp.mode = atoi(e);
+    if (sp.mode == RT_SPLAT_EXACT && (double)total*20.0 > budget) sp.mode = RT_SPLAT_STREAM;
+    if (sp.mode == RT_SPLAT_STREAM && ks > 12) sp.mode = (double)total*20.0 <= budget ? RT_SPLAT_EXACT : RT_SPLAT_ATOMIC;
+    const FrameShape shape = frame_shape(total, spp);
+    size_t need_rec = 0;
+    if (sp.mode == RT_SPLAT_STREAM) {
+        // a resolve every ~32M samples; the ring holds the passes not yet resolved: the chunk,
+        // the claims of the iterations a path can live (about 5 pool fills) and slack
+        const uint32_t per_part = (spp + shape.nparts - 1) / shape.nparts;
+        sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull), per_part);
+        if (const char* e = getenv("RT_SPLAT_CHUNK")) sp.chunk = std::max(1, atoi(e));
+        const unsigned long long lag = (5ull*shape.pool_n + fp.pixels - 1) / fp.pixels;
+        sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, per_part);
+        if (const char* e = getenv("RT_SPLAT_RING")) sp.ring = std::max(1, atoi(e));
+        sp.chunk = std::min(sp.chunk, sp.ring);                      // the planner needs chunk <= ring
+        while (sp.ring > 1 && 20.0*(double)shape.nparts*sp.ring*fp.pixels > budget) {
+            sp.ring = std::max(1u, sp.ring / 2);
+            sp.chunk = std::min(sp.chunk, sp.ring);
+        }
+        need_rec = (size_t)shape.nparts*sp.ring*fp.pixels;
+        if (20.0*(double)need_rec > budget) sp.mode = RT_SPLAT_ATOMIC;
+    }
+    if (sp.mode == RT_SPLAT_EXACT) need_rec = (size_t)total;
+    if (sp.mode != RT_SPLAT_ATOMIC && s->samp_cap < need_rec) {
         if (s->d_samp) (void)hipFree(s->d_samp);
         if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
         s->d_samp = nullptr; s->d_samp_jy = nullptr; s->samp_cap = 0;
-        if (hipMalloc(&s->d_samp, sizeof(float4)*total) != hipSuccess ||
-            hipMalloc(&s->d_samp_jy, sizeof(float)*total) != hipSuccess) {
+        if (hipMalloc(&s->d_samp, sizeof(float4)*need_rec) != hipSuccess ||
+            hipMalloc(&s->d_samp_jy, sizeof(float)*need_rec) != hipSuccess) {
             (void)hipGetLastError();
             if (s->d_samp) (void)hipFree(s->d_samp);
             s->d_samp = nullptr; s->d_samp_jy = nullptr;
-            gather = false;                                   // out of memory: atomic splat
+            sp.mode = RT_SPLAT_ATOMIC;                                 // out of memory
         } else {
-            s->samp_cap = total;
+            s->samp_cap = need_rec;
         }
     }
-    if (gather) {
+    if (sp.mode != RT_SPLAT_ATOMIC) {
         const size_t ntile_all = (size_t)fp.tcx*tcy;
         std::vector<int32_t> base(ntile_all, -1);
         for (size_t i = 0; i < ids.size(); ++i) base[ids[i]] = (int32_t)prefix[i];
@@ -3166,19 +3557,74 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
             s->tile_base_cap = ntile_all;
         }
         HIP_OK(hipMemcpyAsync(s->d_tile_base, base.data(), sizeof(int32_t)*ntile_all, hipMemcpyHostToDevice, stream));
-        HIP_OK(hipStreamSynchronize(stream));     // `base` is a host temporary
         fp.samp_rgbx = s->d_samp;
         fp.samp_jy = s->d_samp_jy;
         fp.tile_base = s->d_tile_base;
-        fp.spp = st->samples_per_pixel;
+        fp.spp = spp;
+        sp.rec = s->d_samp;
+        sp.rec_jy = s->d_samp_jy;
+        std::vector<uint32_t> blocks;
+        std::vector<const float4*> part_ptrs;
+        if (sp.mode == RT_SPLAT_STREAM) {
+            // output blocks whose source region (the block + the filter radius) meets an owned tile
+            const uint32_t nbx = (w + TR_W - 1) / TR_W, nby = (h + TR_H - 1) / TR_H;
+            for (uint32_t by = 0; by < nby; ++by)
+                for (uint32_t bx = 0; bx < nbx; ++bx) {
+                    const int rx0 = std::max<int>((int)(bx*TR_W) - ks, 0), rx1 = std::min<int>((int)(bx*TR_W + TR_W - 1) + ks, (int)w - 1);
+                    const int ry0 = std::max<int>((int)(by*TR_H) - ks, 0), ry1 = std::min<int>((int)(by*TR_H + TR_H - 1) + ks, (int)h - 1);
+                    bool any = false;
+                    for (int ty = ry0 / (int)fp.tile_h; ty <= ry1 / (int)fp.tile_h && !any; ++ty)
+                        for (int tx = rx0 / (int)fp.tile_w; tx <= rx1 / (int)fp.tile_w && !any; ++tx)
+                            any = base[(size_t)ty*fp.tcx + tx] >= 0;
+                    if (any) blocks.push_back(bx | (by << 16));
+                }
+            sp.nblocks = (uint32_t)blocks.size();
+            sp.ksmax = ks <= 2 ? 2 : ks <= 4 ? 4 : 12;
+            sp.lds = tr_lds_bytes(sp.ksmax);
+            const size_t npx = (size_t)w*h;
+            const size_t parts = (size_t)std::max(shape.nparts - 1, 0);
+            if (parts && s->partial_cap < parts*npx) {
+                if (s->d_partials) (void)hipFree(s->d_partials);
+                s->d_partials = nullptr; s->partial_cap = 0;
+                HIP_OK(hipMalloc(&s->d_partials, sizeof(float4)*parts*npx));
+                s->partial_cap = parts*npx;
+            }
+            for (size_t k = 0; k < parts; ++k) part_ptrs.push_back(s->d_partials + k*npx);
+            sp.partials = s->d_partials;
+            const size_t aux = blocks.size() + 2*MAX_PARTITIONS;           // u32 blocks, then the pointers
+            if (s->aux_cap < aux) {
+                if (s->d_aux) (void)hipFree(s->d_aux);
+                s->d_aux = nullptr; s->aux_cap = 0;
+                HIP_OK(hipMalloc(&s->d_aux, sizeof(uint32_t)*aux));
+                s->aux_cap = aux;
+            }
+            uint32_t* d_blocks = s->d_aux + 2*MAX_PARTITIONS;
+            HIP_OK(hipMemcpyAsync(s->d_aux, part_ptrs.data(), sizeof(float4*)*part_ptrs.size(), hipMemcpyHostToDevice, stream));
+            HIP_OK(hipMemcpyAsync(d_blocks, blocks.data(), sizeof(uint32_t)*blocks.size(), hipMemcpyHostToDevice, stream));
+            sp.blocks = d_blocks;
+            sp.part_ptrs = reinterpret_cast<const float4* const*>(s->d_aux);
+            static bool attr_set = false;
+            if (!attr_set) {                      // k_resolve_tiles<12> stages up to 72 KB
+                HIP_OK(hipFuncSetAttribute((const void*)k_resolve_tiles<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tr_lds_bytes(2)));
+                HIP_OK(hipFuncSetAttribute((const void*)k_resolve_tiles<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tr_lds_bytes(4)));
+                HIP_OK(hipFuncSetAttribute((const void*)k_resolve_tiles<12>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tr_lds_bytes(12)));
+                attr_set = true;
+            }
+        }
+        HIP_OK(hipStreamSynchronize(stream));     // `base`, `blocks`, `part_ptrs` are host temporaries
     }
-    err = run_frame(s, st, fp, total, stream, stats);
-    if (err || !gather) return err;
+    err = run_frame(s, st, fp, total, stream, sp, stats);
+    if (err || sp.mode != RT_SPLAT_EXACT) {
+        if (stats && !err) stats->splat_mode = sp.mode;
+        return err;
+    }
     auto t0 = std::chrono::steady_clock::now();
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool prof_resolve = (g_profiling >> RT_KERNEL_RESOLVE) & 1u;
     if (prof_resolve) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
-    const bool tall = fp.pixels >= RES_TALL_PIXELS;
+    uint32_t tall_px = RES_TALL_PIXELS;
+    if (const char* e = getenv("RT_RES_TALL_PIXELS")) tall_px = (uint32_t)strtoul(e, nullptr, 0);   // tests: both heights
+    const bool tall = fp.pixels >= tall_px;
     const int rry = tall ? RT_RES_RY_TALL : RT_RES_RY;
     dim3 rgrid((w + RES_BX - 1) / RES_BX, (h + RES_BY*rry - 1) / (RES_BY*rry));
     if (tall) k_resolve<RT_RES_RY_TALL><<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
@@ -3199,6 +3645,7 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     }
 #endif
     if (stats) {
+        stats->splat_mode = sp.mode;
         stats->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         if (prof_resolve) {
             float ms = 0.0f;
@@ -3228,6 +3675,29 @@ int rt_render(rt_scene* s, const rt_camera* camera, const rt_settings* st, const
     return err;
 }
 
+int rt_render_picture(rt_scene* s, const rt_camera* camera, const rt_settings* st, const rt_filter_cache* filter,
+                      const rt_tile_set* tiles, uint32_t total_frame_index, uint32_t w, uint32_t h,
+                      const rt_post_settings* post, uint32_t* out_bgra, rt_stats* stats) {
+    if (!s || !post || !out_bgra || !w || !h) { set_error("null argument"); return RT_ERROR_INVALID; }
+    HIP_OK(hipSetDevice(s->device));
+    const size_t n = (size_t)w*h;
+    float* d_px = nullptr;
+    uint32_t* d_out = nullptr;
+    HIP_OK(hipMalloc(&d_px, 16*n));
+    if (hipMalloc(&d_out, 4*n) != hipSuccess) { (void)hipFree(d_px); set_error("hipMalloc"); return RT_ERROR_OUT_OF_MEMORY; }
+    int err = RT_OK;
+    if (hipMemset(d_px, 0, 16*n) != hipSuccess) { set_error("hipMemset"); err = RT_ERROR_DEVICE; }
+    // discard_current_render + reset: a fresh buffer, frame_count 0 (RT/raytracer.cpp:2037-2041, :711-719)
+    if (!err) err = rt_render_device(s, camera, st, filter, tiles, total_frame_index, w, h, 0u, d_px, nullptr, stats);
+    // the frame completes with settings and camera unchanged, so render_all_tiles has moved
+    // total_frame_index on (:720-724) before the output pass picks its dither texture (:2108)
+    if (!err) err = rt_postprocess_device(s->device, d_px, w, h, post, total_frame_index + 1u, d_out, nullptr);
+    if (!err && hipMemcpy(out_bgra, d_out, 4*n, hipMemcpyDeviceToHost) != hipSuccess) { set_error("copy out"); err = RT_ERROR_DEVICE; }
+    (void)hipFree(d_px);
+    (void)hipFree(d_out);
+    return err;
+}
+
 int rt_trace_samples(rt_scene* s, const rt_camera* camera, const rt_settings* st,
                      uint32_t w, uint32_t h, uint32_t tile_w, uint32_t tile_h,
                      uint32_t frame_count, uint32_t total_frame_index,
@@ -3252,7 +3722,7 @@ int rt_trace_samples(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.tile_w = tile_w; fp.tile_h = tile_h; fp.tcx = (w + tile_w - 1) / tile_w;
     fp.list_xy = d_xy; fp.list_s = d_s; fp.list_out = d_out;
     fill_camera(fp, camera);
-    err = run_frame(s, st, fp, count, nullptr, stats);
+    err = run_frame(s, st, fp, count, nullptr, SplatCfg{}, stats);
     if (!err && hipMemcpy(out, d_out, 20*(size_t)count, hipMemcpyDeviceToHost) != hipSuccess) { set_error("copy out"); err = RT_ERROR_DEVICE; }
     (void)hipFree(d_xy); (void)hipFree(d_s); (void)hipFree(d_out);
     return err;

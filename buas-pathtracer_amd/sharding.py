@@ -1,11 +1,16 @@
 """Multi-GPU decomposition of a frame.
 
-Tile t of the frame is rendered by rank t % world (interleaved for load
-balance, the reference's 64x64 tiles), every rank accumulates into a full-frame
-float4 buffer in which only its tiles' splats are non-zero, and one sum
-reduction over the ranks (RCCL over xGMI on MI355X, gloo in the CPU tests)
-produces the frame.  Samples are keyed by (frame, tile, pixel, sample), so the
-result does not depend on the number of ranks beyond float summation order.
+Tile t of the frame is rendered by rank t % world (interleaved for load balance, the
+reference's 64x64 tiles).  Every rank renders its share of the frame into a full-frame
+float4 buffer that starts the frame at zero (only its tiles' splats are non-zero), one sum
+reduction over the ranks (RCCL over xGMI on MI355X, gloo in the CPU tests) combines the
+shares in rank 0, and rank 0 adds the frame to its accumulation buffer.  Samples are keyed by
+(frame, tile, pixel, sample), so the result does not depend on the number of ranks beyond
+float summation order.
+
+Progressive accumulation (frame_count > 0, RT/raytracer.cpp:720-724) is therefore safe: the
+accumulation buffer of a rank other than 0 is never read or changed, and rank 0's earlier
+frames are reduced with nobody else's.
 """
 
 
@@ -16,12 +21,18 @@ def owned_tiles(w, h, tile_w, tile_h, rank, world):
     return [t for t in range(tcx * tcy - 1, -1, -1) if t % world == rank]
 
 
-def render_frame_sharded(render_shard, accum, rank, world, group=None):
-    """render_shard(shard_index, shard_count, accum) adds this rank's tiles into
-    `accum` (a torch tensor); the frame is then sum-reduced into rank 0's buffer.
-    Returns the render_shard result (per-rank stats)."""
+def render_frame_sharded(render_shard, accum, rank, world, group=None, scratch=None):
+    """render_shard(shard_index, shard_count, buf) ADDS this rank's tiles of one frame into
+    `buf` (a torch tensor shaped like `accum`).  With world > 1 the frame is rendered into
+    `scratch` (zeroed here; allocated if None), sum-reduced into rank 0 and added to rank 0's
+    `accum`; the other ranks' `accum` is left untouched.  Returns the render_shard result."""
+    if world == 1:
+        return render_shard(rank, world, accum)
     import torch.distributed as dist
-    stats = render_shard(rank, world, accum)
-    if world > 1:
-        dist.reduce(accum, dst=0, group=group)
+    buf = scratch if scratch is not None else accum.new_zeros(accum.shape)
+    buf.zero_()
+    stats = render_shard(rank, world, buf)
+    dist.reduce(buf, dst=0, group=group)
+    if rank == 0:
+        accum.add_(buf)
     return stats

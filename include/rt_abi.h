@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status */
 enum rt_status {
@@ -218,6 +218,8 @@ typedef struct rt_stats {
     /* rays handed to the trace kernels (closest, shadow): the rest were settled by
        the planes / top-level root test where they were made (GPU only) */
     uint64_t traced_rays[2];
+    int32_t  splat_mode;            /* rt_splat_mode the frame used (rt_render / rt_render_device) */
+    int32_t  reserved;
 } rt_stats;
 
 typedef struct rt_ray_query {       /* debug/parity entry: one ray for rt_debug_intersect */
@@ -264,6 +266,16 @@ int rt_render_device(rt_scene* scene, const rt_camera* camera, const rt_settings
                      const rt_filter_cache* filter, const rt_tile_set* tiles,
                      uint32_t total_frame_index, uint32_t w, uint32_t h, uint32_t frame_count,
                      float* d_pixels, void* hip_stream, rt_stats* stats);
+
+/* The frame of the reference's "Take picture" (RT/raytracer.cpp:2031-2048, :2089-2176):
+ * renders total_frame_index's frame of settings->samples_per_pixel samples per pixel
+ * into a fresh device buffer (frame_count 0), then runs the output pass on the device
+ * (rt_postprocess_device) with the dither texture of total_frame_index + 1 -- the frame
+ * completing advances the index before the output pass reads it (:720-724, :2108) -- and
+ * copies the BGRA8 picture (w*h u32, host) out.  write_bitmap is the caller's. */
+int rt_render_picture(rt_scene* scene, const rt_camera* camera, const rt_settings* settings,
+                      const rt_filter_cache* filter, const rt_tile_set* tiles, uint32_t total_frame_index,
+                      uint32_t w, uint32_t h, const rt_post_settings* post, uint32_t* out_bgra, rt_stats* stats);
 
 /* Parity entry: integrate an explicit list of samples (pixel x,y + sample
  * offset s, canonical index = frame_count + s) with RT_RNG_PER_SAMPLE and
@@ -326,6 +338,24 @@ int rt_set_profiling_stages(uint32_t mask);
 /* Size of the in-flight path pool per partition (paths resident in HBM); 0 = default:
  * an eighth of the partition's samples, clamped to [2^21, 3 x 2^21]. */
 int rt_set_path_pool(uint32_t paths);
+
+/* How samples reach the accumulation buffer (splat_filter, RT/raytracer.cpp:187-259).
+ *   RT_SPLAT_STREAM (default): each sample's 20-byte record goes to a ring of sample passes
+ *     in HBM; k_resolve_tiles gathers completed passes into the buffer while the frame still
+ *     renders, reading every record once.  Deterministic (the same bits whatever the timing
+ *     or the split of passes between launches); equal to the reference's frame up to float
+ *     summation order.
+ *   RT_SPLAT_EXACT: records of the whole frame, then one gather in the reference's
+ *     single-threaded order (tiles descending, pixels, samples): bit-identical to the
+ *     reference order.  Over the HBM budget it renders as RT_SPLAT_STREAM.
+ *   RT_SPLAT_ATOMIC: float atomics into the buffer (order-dependent last bits).
+ * The mode a frame used is reported in rt_stats::splat_mode. */
+enum rt_splat_mode {
+    RT_SPLAT_STREAM = 0,
+    RT_SPLAT_EXACT  = 1,
+    RT_SPLAT_ATOMIC = 2,
+};
+int rt_set_splat_mode(int mode);
 
 /* discard_current_render (RT/raytracer.cpp:686-690): polled between wavefront
  * iterations; the render in flight returns RT_ERROR_CANCELLED. */

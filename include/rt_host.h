@@ -124,18 +124,22 @@ uint32_t rth_generate_mesh(uint32_t target_triangles, uint32_t seed, rt_v3* out_
 int      rth_write_synthetic_obj(const char* path, uint32_t target_triangles, uint32_t seed);
 int      rth_write_synthetic_hdr(const char* path, uint32_t w, uint32_t h, uint32_t seed);
 
-/* Output (RT/raytracer.cpp:2103-2173 without the blue-noise TPDF dither, and
- * RT/assets.cpp:693-724). */
+/* Host preview of the output pass (RT/raytracer.cpp:2103-2173 with a flat 0.5 in place of
+ * the blue-noise TPDF dither; the picture path uses the device pass, rt_postprocess*), and
+ * write_bitmap (RT/assets.cpp:693-724): top-down 32-bit BGRA.  rth_read_bitmap reads such a
+ * file back (tests). */
 void rth_resolve_bgra8(const rt_accumulation_buffer* accum, const rth_post_settings* post, uint32_t* out_bgra);
 int  rth_write_bitmap(const char* path, const uint32_t* bgra, uint32_t w, uint32_t h);
+int  rth_read_bitmap(const char* path, uint32_t* bgra, uint32_t w, uint32_t h);
 
-/* Render-to-bitmap entry point ("Take picture", RT/raytracer.cpp:2031-2048, 2175-2185):
- * renders `spp` samples per pixel of the scene through rt_render on `device`
- * into a fresh accumulation buffer and writes the BMP.  seconds_out may be NULL. */
+/* Render-to-bitmap entry point ("Take picture", RT/raytracer.cpp:2031-2048, 2089-2185):
+ * renders `spp` samples per pixel of frame `total_frame_index` on `device` into a fresh
+ * accumulation buffer, runs the reference's output pass with its TPDF dither on the device
+ * (rt_render_picture) and writes the BMP.  stats_out may be NULL. */
 int rth_take_picture(rth_scene* s, const rt_camera* camera, const rt_settings* settings,
                      const rt_filter_cache* filter, const rth_post_settings* post,
-                     uint32_t w, uint32_t h, uint32_t spp, int device, const char* bmp_path,
-                     rt_stats* stats_out);
+                     uint32_t w, uint32_t h, uint32_t spp, uint32_t total_frame_index, int device,
+                     const char* bmp_path, rt_stats* stats_out);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,14 @@
-"""World-size-2 gloo test of the multi-GPU decomposition on CPU: each rank
-renders its interleaved tiles (t % 2 == rank) with the CPU oracle into a full
-frame buffer, the buffers are sum-reduced with gloo (RCCL on the GPU box), and
-the result must equal the single-rank frame up to float summation order."""
+"""World-size-2 gloo tests of the multi-GPU decomposition (sharding.render_frame_sharded, the
+flow bench.py runs with RCCL): each rank renders its interleaved tiles (t % 2 == rank) into a
+zeroed full-frame buffer, the buffers are sum-reduced into rank 0, which adds the frame to its
+accumulation buffer.  Two progressive frames are rendered, and rank 1 starts with garbage in
+its accumulation buffer: the result must equal the single-rank accumulation of both frames up
+to float summation order, and rank 1's buffer must be left untouched.
+
+The CPU test renders the shards with the oracle; the GPU test renders them with the HIP path
+(rt_render_device into a torch tensor on cuda:0, both ranks on the one GPU of the box) and
+reduces with gloo on host copies (RCCL cannot put two ranks on one device).
+"""
 import os
 import socket
 
@@ -12,6 +19,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 W, H = 128, 96
+SPP = 4
 
 
 def _free_port():
@@ -20,7 +28,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, backend):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, here)
@@ -32,38 +40,76 @@ def _worker(rank, world, port, out_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     scene, cam, st, fc, post = rt.load_preset("c1", W, H)
-    st.samples_per_pixel = 4
+    st.samples_per_pixel = SPP
     accum = torch.zeros((H, W, 4), dtype=torch.float32)
+    if rank:
+        accum.fill_(123.0)                 # a rank other than 0 never reads or changes its buffer
+    dev = rt.DeviceScene(scene, 0) if backend == "gpu" else None
+    frame = {"fc": 0, "tfi": 0}
 
     def render_shard(shard_index, shard_count, buf):
-        a = buf.numpy()
-        _, stats = ob.render(scene.desc(), cam, st, fc, W, H, rng_mode=0, threads=2, accum=a,
-                             shard_index=shard_index, shard_count=shard_count)
+        if dev is None:
+            _, stats = ob.render(scene.desc(), cam, st, fc, W, H, rng_mode=0, threads=2, accum=buf.numpy(),
+                                 shard_index=shard_index, shard_count=shard_count,
+                                 frame_count=frame["fc"], total_frame_index=frame["tfi"])
+        else:
+            d = buf.to("cuda:0")
+            stats = dev.render_device(cam, st, fc, W, H, d.data_ptr(), frame_count=frame["fc"],
+                                      total_frame_index=frame["tfi"], shard_index=shard_index,
+                                      shard_count=shard_count)
+            torch.cuda.synchronize(0)
+            buf.copy_(d.cpu())
         return stats.samples
 
-    samples = render_frame_sharded(render_shard, accum, rank, world)
+    samples = 0
+    for f in range(2):                      # two progressive frames (RT/raytracer.cpp:720-724)
+        frame["fc"], frame["tfi"] = f * SPP, f
+        samples += render_frame_sharded(render_shard, accum, rank, world)
     n = torch.tensor([samples], dtype=torch.float64)
     dist.all_reduce(n)
     if rank == 0:
         np.save(out_path, accum.numpy())
-        with open(out_path + ".n", "w") as f:
-            f.write(str(int(n.item())))
+        with open(out_path + ".n", "w") as fh:
+            fh.write(str(int(n.item())))
+    else:
+        assert torch.all(accum == 123.0)
     assert len(owned_tiles(W, H, 64, 64, rank, world)) >= 1
+    if dev is not None:
+        dev.close()
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_matches_single(rt, tmp_path):
+def _single(rt):
     import oracle_binding as ob
-    out = str(tmp_path / "frame.npy")
-    mp.spawn(_worker, args=(2, _free_port(), out), nprocs=2, join=True)
-    reduced = np.load(out)
     scene, cam, st, fc, post = rt.load_preset("c1", W, H)
-    st.samples_per_pixel = 4
-    full, stats = ob.render(scene.desc(), cam, st, fc, W, H, rng_mode=0, threads=2)
-    assert int(open(out + ".n").read()) == stats.samples == W * H * 4
+    st.samples_per_pixel = SPP
+    full = np.zeros((H, W, 4), np.float32)
+    n = 0
+    for f in range(2):
+        _, stats = ob.render(scene.desc(), cam, st, fc, W, H, rng_mode=0, threads=2, accum=full,
+                             frame_count=f * SPP, total_frame_index=f)
+        n += stats.samples
+    return full, n
+
+
+def _run(rt, tmp_path, backend):
+    out = str(tmp_path / "frame.npy")
+    mp.spawn(_worker, args=(2, _free_port(), out, backend), nprocs=2, join=True)
+    reduced = np.load(out)
+    full, n = _single(rt)
+    assert int(open(out + ".n").read()) == n == 2 * W * H * SPP
     err = np.linalg.norm((reduced - full).astype(np.float64)) / np.linalg.norm(full.astype(np.float64))
-    assert err <= 1e-6
+    assert err <= 1e-5, err
+
+
+def test_two_rank_gloo_matches_single(rt, tmp_path):
+    _run(rt, tmp_path, "oracle")
+
+
+@pytest.mark.gpu
+def test_two_rank_gloo_hip_shards_match_single(rt, tmp_path):
+    _run(rt, tmp_path, "gpu")
 
 
 def test_owned_tiles_partition(rt):

@@ -1,0 +1,191 @@
+"""GPU parity for the configurations and options tests/test_gpu_parity.py does not reach:
+
+* C2 (Cornell box + the 70k-triangle mesh, no environment map, 64 spp): samples and frames;
+* every reconstruction filter of g_filters (RT/reconstruction_filters.cpp:97-106) in both
+  deterministic splats: Box, Gaussian 3 / 12, Mitchell-Netravali, Lanczos 3 / 4 / 6 / 12
+  (radius 12 exercises k_resolve_tiles' widest staging);
+* the bokeh polygon (f_factor != 0, RT/raytracer.cpp:86-94) with DOF;
+* the render-to-bitmap entry point (rth_take_picture -> rt_render_picture -> write_bitmap,
+  RT/raytracer.cpp:2031-2185) against the oracle's output pass;
+* rt_cancel in the middle of a frame (discard_current_render, RT/raytracer.cpp:686-690) and a
+  bit-exact frame right after it;
+* frames sharded over 2, 4 and 8 ranks (tiles t % N) summing to the single-rank frame, in the
+  streaming splat (each rank resolves only the blocks its tiles reach) and the exact one.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+from test_gpu_parity import REPORT, rel_l2, _sample_list
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c2small(rt):
+    scene, cam, st, fc, post = rt.load_preset("c2", 192, 108)
+    dev = rt.DeviceScene(scene, 0)
+    yield rt, scene, cam, st, fc, post, dev
+    dev.close()
+
+
+def test_c2_trace_samples_bitwise(c2small):
+    rt, scene, cam, st, fc, post, dev = c2small
+    rng = np.random.default_rng(21)
+    xy, s = _sample_list(rng, 192, 108, 20000, st.samples_per_pixel)
+    gpu, gs = dev.trace_samples(cam, st, 192, 108, xy, s)
+    cpu, cs = ob.trace_samples(scene.desc(), cam, st, 192, 108, xy, s)
+    same = np.all((gpu == cpu) | (np.isnan(gpu) & np.isnan(cpu)), axis=1).mean()
+    REPORT["trace_samples_c2small"] = {"samples": int(len(xy)), "bit_exact_fraction": float(same)}
+    assert same >= 0.999
+    assert gs.closest_hit_rays == cs.closest_hit_rays or same < 1.0
+
+
+@pytest.mark.parametrize("mode", ["exact", "stream"])
+def test_c2_frame(c2small, mode):
+    rt, scene, cam, st, fc, post, dev = c2small
+    m = rt.abi.RT_SPLAT_EXACT if mode == "exact" else rt.abi.RT_SPLAT_STREAM
+    with rt.splat_mode(m):
+        gpu, gs = dev.render(cam, st, fc, 192, 108)
+    cpu, cs = ob.render(scene.desc(), cam, st, fc, 192, 108, rng_mode=0, threads=1)
+    REPORT[f"frame_c2small_{mode}"] = {"rel_l2": rel_l2(gpu, cpu), "bit_identical": bool(np.array_equal(gpu, cpu))}
+    assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
+    if mode == "exact":
+        assert np.all(gpu == cpu, axis=2).mean() >= 0.999
+        assert rel_l2(gpu, cpu) <= 1e-6
+    else:
+        assert rel_l2(gpu, cpu) <= 1e-5
+
+
+FILTERS = ["Box", "Gaussian 3", "Gaussian 12", "Mitchell Netravali", "Lanczos 3", "Lanczos 4", "Lanczos 6",
+           "Lanczos 12"]
+
+
+@pytest.mark.parametrize("name", FILTERS)
+def test_every_reconstruction_filter(rt, name):
+    """Each g_filters entry through both deterministic splats against the oracle's
+    single-threaded splat_filter (C1 at 128x96, 8 spp; Lanczos lobes give negative weights)."""
+    scene, cam, st, fc, post = rt.load_preset("c1", 128, 96)
+    st.samples_per_pixel = 8
+    filt = rt.load_reconstruction_kernel(name)
+    ref = ob.load()
+    ofc = type(filt)()
+    assert ref.oracle_load_filter(name.encode(), ofc) == 0
+    assert (ofc.kernel_size, ofc.cache_size) == (filt.kernel_size, filt.cache_size)
+    assert np.array_equal(np.ctypeslib.as_array(ofc.cache), np.ctypeslib.as_array(filt.cache))
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+            exact, es = dev.render(cam, st, filt, 128, 96)
+        stream, ss = dev.render(cam, st, filt, 128, 96)
+    finally:
+        dev.close()
+    cpu, _ = ob.render(scene.desc(), cam, st, filt, 128, 96, rng_mode=0, threads=1)
+    REPORT[f"filter_{name}"] = {"exact_pixels_bit_identical": float(np.all(exact == cpu, axis=2).mean()),
+                                "stream_rel_l2": rel_l2(stream, cpu), "stream_mode": int(ss.splat_mode)}
+    assert es.splat_mode == rt.abi.RT_SPLAT_EXACT and ss.splat_mode == rt.abi.RT_SPLAT_STREAM
+    assert np.all(exact == cpu, axis=2).mean() >= 0.999
+    assert rel_l2(exact, cpu) <= 1e-6
+    assert rel_l2(stream, cpu) <= 1e-5
+
+
+@pytest.mark.parametrize("f_factor,edges", [(0.5, 6.0), (1.0, 5.0), (0.25, 3.0)])
+def test_bokeh_polygon(rt, f_factor, edges):
+    """transform_bokeh_sample with f_factor != 0 (RT/raytracer.cpp:86-94): the polygonal
+    aperture of diaphragm_edges blades, rotated by f * phi_shutter_max, on C3's DOF camera."""
+    scene, cam, st, fc, post = rt.load_preset("c3", 192, 108)
+    assert cam.lens_radius > 0
+    st.f_factor = f_factor
+    st.diaphragm_edges = edges
+    st.samples_per_pixel = 32
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        rng = np.random.default_rng(9)
+        xy, s = _sample_list(rng, 192, 108, 20000, st.samples_per_pixel)
+        gpu, _ = dev.trace_samples(cam, st, 192, 108, xy, s)
+        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+            frame, _ = dev.render(cam, st, fc, 192, 108)
+    finally:
+        dev.close()
+    cpu, _ = ob.trace_samples(scene.desc(), cam, st, 192, 108, xy, s)
+    same = np.all((gpu == cpu) | (np.isnan(gpu) & np.isnan(cpu)), axis=1).mean()
+    cframe, _ = ob.render(scene.desc(), cam, st, fc, 192, 108, rng_mode=0, threads=1)
+    REPORT[f"bokeh_f{f_factor}_n{edges}"] = {"bit_exact_fraction": float(same), "frame_rel_l2": rel_l2(frame, cframe)}
+    assert same >= 0.999
+    assert rel_l2(frame, cframe) <= 1e-6
+
+
+@pytest.mark.parametrize("mode", ["exact", "stream"])
+def test_take_picture_bitmap(rt, tmp_path, mode):
+    """rth_take_picture renders frame T on the device, runs the output pass with the dither of
+    frame T + 1 and writes the BMP: its pixels equal oracle_postprocess of the same frame."""
+    w, h, T = 192, 108, 5
+    scene, cam, st, fc, post = rt.load_preset("c3", w, h)
+    path = tmp_path / "picture.bmp"
+    m = rt.abi.RT_SPLAT_EXACT if mode == "exact" else rt.abi.RT_SPLAT_STREAM
+    with rt.splat_mode(m):
+        stats = rt.take_picture(scene, cam, st, fc, post, w, h, 16, path, total_frame_index=T)
+        st.samples_per_pixel = 16
+        dev = rt.DeviceScene(scene, 0)
+        try:
+            frame, _ = dev.render(cam, st, fc, w, h, total_frame_index=T)
+        finally:
+            dev.close()
+    pic = rt.read_bitmap(path, w, h)
+    assert stats.samples == w * h * 16
+    assert np.array_equal(pic, ob.postprocess(frame, post, total_frame_index=T + 1))
+    if mode == "exact":
+        cpu, _ = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1, total_frame_index=T)
+        ref = ob.postprocess(cpu, post, total_frame_index=T + 1)
+        REPORT["take_picture_exact"] = {"pixels_equal": float((pic == ref).mean())}
+        assert (pic == ref).mean() >= 0.999
+
+
+def test_cancel_mid_frame(rt):
+    """rt_cancel from another thread while a long frame renders returns RT_ERROR_CANCELLED
+    (after the partitions' in-flight work has drained), and the next frame is bit-exact."""
+    scene, cam, st, fc, post = rt.load_preset("c3", 1920, 1080)
+    st.samples_per_pixel = 1024                      # ~1.2 s: the cancel lands mid-frame
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        timer = threading.Timer(0.15, dev.cancel)
+        timer.start()
+        with pytest.raises(rt.RenderError) as ei:
+            dev.render(cam, st, fc, 1920, 1080)
+        timer.join()
+        assert ei.value.code == rt.abi.RT_ERROR_CANCELLED
+        small = type(st).from_buffer_copy(st)
+        small.samples_per_pixel = 16
+        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+            gpu, gs = dev.render(cam, small, fc, 192, 108)
+    finally:
+        dev.close()
+    cpu, cs = ob.render(scene.desc(), cam, small, fc, 192, 108, rng_mode=0, threads=1)
+    REPORT["cancel_then_render"] = {"bit_identical": bool(np.array_equal(gpu, cpu))}
+    assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
+    assert np.all(gpu == cpu, axis=2).mean() >= 0.999
+
+
+@pytest.mark.parametrize("n", [2, 4, 8])
+@pytest.mark.parametrize("mode", ["stream", "exact"])
+def test_sharded_frames_sum(rt, n, mode):
+    """Ranks' shares (tiles t % N, each rendered as a whole frame of its own) sum to the
+    single-rank frame: the per-rank sample keys make the shares disjoint, and every filter
+    footprint crossing a tile border lands in the right buffer."""
+    scene, cam, st, fc, post = rt.load_preset("c3", 320, 200)
+    st.samples_per_pixel = 16
+    m = rt.abi.RT_SPLAT_EXACT if mode == "exact" else rt.abi.RT_SPLAT_STREAM
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        with rt.splat_mode(m):
+            full, fs = dev.render(cam, st, fc, 320, 200)
+            parts = [dev.render(cam, st, fc, 320, 200, shard_index=r, shard_count=n) for r in range(n)]
+    finally:
+        dev.close()
+    total = sum(p[0].astype(np.float64) for p in parts)
+    REPORT[f"sharded_{mode}_{n}"] = {"rel_l2": rel_l2(total, full)}
+    assert sum(p[1].samples for p in parts) == fs.samples
+    assert sum(p[1].closest_hit_rays for p in parts) == fs.closest_hit_rays
+    assert rel_l2(total, full) <= 1e-5

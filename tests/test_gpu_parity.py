@@ -193,20 +193,76 @@ def test_frame_rel_l2(which, w, h, request):
     assert abs(int(gstats.shadow_rays) - int(cstats.shadow_rays)) <= 1e-4 * cstats.shadow_rays
 
 
+@pytest.mark.parametrize("strip", ["4row", "8row"])
 @pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108), ("c4small", 192, 108),
                                        ("c5small", 96, 54), ("c1uniform", 128, 128)])
-def test_frame_bitwise_vs_reference_order(which, w, h, request):
-    """k_resolve sums each pixel's contributions in the single-threaded reference
-    order, so the GPU frame equals the oracle's threads=1 frame bit for bit
-    wherever every contributing sample is bit-exact (>= 99.9 % of pixels)."""
+def test_frame_bitwise_vs_reference_order(which, w, h, strip, request, monkeypatch):
+    """The exact splat (RT_SPLAT_EXACT, k_resolve) sums each pixel's contributions in the
+    single-threaded reference order, so the GPU frame equals the oracle's threads=1 frame
+    bit for bit wherever every contributing sample is bit-exact (>= 99.9 % of pixels).
+    Both strip heights of k_resolve run: 4 rows, and the 8 rows whole-frame shards of
+    >= 1.6M pixels use (forced here by RT_RES_TALL_PIXELS=1)."""
     rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
-    gpu, _ = dev.render(cam, st, fc, w, h)
+    monkeypatch.setenv("RT_RES_TALL_PIXELS", "1" if strip == "8row" else "4294967295")
+    with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+        gpu, gs = dev.render(cam, st, fc, w, h)
+    assert gs.splat_mode == rt.abi.RT_SPLAT_EXACT
     cpu, _ = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1)
     same = np.all(gpu == cpu, axis=2).mean()
-    REPORT[f"frame_bitwise_{which}"] = {"pixels_bit_identical": float(same), "rel_l2": rel_l2(gpu, cpu),
-                                        "frame_equal": bool(np.array_equal(gpu, cpu))}
+    REPORT[f"frame_bitwise_{which}_{strip}"] = {"pixels_bit_identical": float(same), "rel_l2": rel_l2(gpu, cpu),
+                                                "frame_equal": bool(np.array_equal(gpu, cpu))}
     assert same >= 0.999
     assert rel_l2(gpu, cpu) <= 1e-6
+
+
+@pytest.mark.parametrize("which,w,h", [("c1", 256, 256), ("c3small", 192, 108), ("c4small", 192, 108),
+                                       ("c5small", 96, 54)])
+def test_stream_splat_vs_reference_order(which, w, h, request):
+    """The streaming splat (the default, k_resolve_tiles) sums pass by pass: the frame
+    equals the reference-order frame up to float summation order (rel L2 <= 1e-5), with
+    the same sample and ray counts."""
+    rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
+    gpu, gs = dev.render(cam, st, fc, w, h)
+    assert gs.splat_mode == rt.abi.RT_SPLAT_STREAM
+    cpu, cs = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1)
+    err = rel_l2(gpu, cpu)
+    wdiff = float(np.abs(gpu[..., 3] - cpu[..., 3]).max())
+    REPORT[f"frame_stream_{which}"] = {"rel_l2": err, "max_abs_weight_diff": wdiff}
+    assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
+    assert err <= 1e-5
+    assert np.isfinite(gpu).all() == np.isfinite(cpu).all()
+
+
+@pytest.mark.parametrize("env", [{"RT_SPLAT_CHUNK": "1", "RT_SPLAT_RING": "1"}, {"RT_SPLAT_CHUNK": "3", "RT_SPLAT_RING": "5"},
+                                 {"RT_SPLAT_CHUNK": "1000"}])
+def test_stream_splat_deterministic_in_chunking(c3small, env, monkeypatch):
+    """k_resolve_tiles' result does not depend on how the passes are split between its
+    launches or on the record ring's size (a one-pass ring throttles the sample claims):
+    the frames are bit-identical to the default streaming frame, and to a second run."""
+    rt, scene, cam, st, fc, dev = c3small
+    st = type(st).from_buffer_copy(st)
+    st.samples_per_pixel = 24
+    ref, rs = dev.render(cam, st, fc, 192, 108)
+    again, _ = dev.render(cam, st, fc, 192, 108)
+    assert np.array_equal(ref, again)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    got, gs = dev.render(cam, st, fc, 192, 108)
+    REPORT["stream_chunking_" + "_".join(f"{k}={v}" for k, v in env.items())] = {
+        "frame_equal": bool(np.array_equal(ref, got)), "iterations": [int(rs.iterations), int(gs.iterations)]}
+    assert (gs.closest_hit_rays, gs.shadow_rays) == (rs.closest_hit_rays, rs.shadow_rays)
+    assert np.array_equal(ref, got)
+
+
+def test_stream_splat_box_filter_bit_exact(c1, monkeypatch):
+    """With one partition the streaming splat of the box filter adds each pixel's samples in
+    sample order, the reference's order: bit-identical to the oracle's frame."""
+    rt, scene, cam, st, fc, dev = c1
+    monkeypatch.setenv("RT_PARTITIONS", "1")
+    box = rt.load_reconstruction_kernel("Box")
+    gpu, _ = dev.render(cam, st, box, 256, 256)
+    cpu, _ = ob.render(scene.desc(), cam, st, box, 256, 256, rng_mode=0, threads=1)
+    assert np.array_equal(gpu, cpu)
 
 
 def test_sharded_frames_sum_to_full(c1):
@@ -241,7 +297,8 @@ def test_golden_frame_hash(rt):
     gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))["c1_64x64_frame"]
     scene, cam, st, fc, post = rt.load_preset("c1", 64, 64)
     dev = rt.DeviceScene(scene, 0)
-    acc, stats = dev.render(cam, st, fc, 64, 64)
+    with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+        acc, stats = dev.render(cam, st, fc, 64, 64)
     dev.close()
     REPORT["golden_c1_64"] = {"sha256_equal": hashlib.sha256(acc.tobytes()).hexdigest() == gold["sha256"],
                               "rays": [int(stats.closest_hit_rays), int(stats.shadow_rays)],
@@ -297,18 +354,24 @@ def test_top_level_paths(rt, env, monkeypatch):
     assert gstats.closest_hit_rays == cstats.closest_hit_rays or same < 1.0
 
 
-def test_atomic_splat_fallback(rt, monkeypatch):
-    """Frames whose sample records exceed the HBM budget splat with float atomics
-    (k_splat): the same image up to float summation order."""
-    monkeypatch.setenv("RT_SAMPLE_BUDGET_GB", "0")
+@pytest.mark.parametrize("how", ["budget", "mode"])
+def test_atomic_splat_fallback(rt, monkeypatch, how):
+    """Frames whose sample records exceed the HBM budget (even a one-pass ring), or
+    RT_SPLAT_ATOMIC, splat with float atomics: the same image up to float summation order."""
     scene, cam, st, fc, post = rt.load_preset("c1", 128, 128)
     dev = rt.DeviceScene(scene, 0)
     try:
-        gpu, stats = dev.render(cam, st, fc, 128, 128)
+        if how == "budget":
+            monkeypatch.setenv("RT_SAMPLE_BUDGET_GB", "0")
+            gpu, stats = dev.render(cam, st, fc, 128, 128)
+        else:
+            with rt.splat_mode(rt.abi.RT_SPLAT_ATOMIC):
+                gpu, stats = dev.render(cam, st, fc, 128, 128)
+        assert stats.splat_mode == rt.abi.RT_SPLAT_ATOMIC
     finally:
         dev.close()
     cpu, cstats = ob.render(scene.desc(), cam, st, fc, 128, 128, rng_mode=0, threads=8)
-    REPORT["atomic_splat_c1_128"] = {"rel_l2": rel_l2(gpu, cpu)}
+    REPORT[f"atomic_splat_c1_128_{how}"] = {"rel_l2": rel_l2(gpu, cpu)}
     assert (stats.closest_hit_rays, stats.shadow_rays) == (cstats.closest_hit_rays, cstats.shadow_rays)
     assert rel_l2(gpu, cpu) <= 1e-5
 

@@ -1,0 +1,99 @@
+"""Noise-aware comparison of the GPU's per-sample RNG with the reference's tile stream.
+
+The reference draws every random number of a 64x64 tile from one xorshift RandomSeries seeded
+from (total_frame_index, frame_count, tile) and consumed serially pixel by pixel, sample by
+sample (RT/raytracer.cpp:588-593) -- a stream no parallel renderer can reproduce.  The GPU
+seeds a RandomSeries per sample from the same tile seed plus the pixel and the sample index
+(RT_RNG_PER_SAMPLE) and keeps the reference's draw order inside a sample.  Both
+are unbiased estimators of the same pixel integrals, so their frames agree in distribution:
+
+* the frame sums sum(rgb) and sum(w) over 8 frames (total_frame_index 0..7) have means within
+  K sigma of each other, sigma estimated from the 8 frames of each side;
+* the same holds per 64x64 tile (the unit of the reference's stream), and for the closest-hit
+  and shadow rays per sample.
+
+The CPU test runs the oracle in both modes (RT_RNG_PER_SAMPLE is bit-exact with the GPU,
+tests/test_gpu_parity.py); the GPU tests compare the GPU's own frames with the oracle's
+tile-stream frames (the oracle's tile-stream mode reproduces the reference's C1 output exactly,
+tests/test_oracle_pins.py).
+"""
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+
+K = 4.5          # sigma bound; with ~100 tile comparisons a false alarm at 4.5 sigma is < 1e-3
+SEEDS = 8
+
+
+def _frames(render, seeds=SEEDS):
+    out = []
+    for t in range(seeds):
+        frame, stats = render(t)
+        out.append((frame.astype(np.float64), stats.closest_hit_rays / stats.samples, stats.shadow_rays / stats.samples))
+    return out
+
+
+def _tile_sums(frame, tile=64):
+    h, w, _ = frame.shape
+    ty, tx = (h + tile - 1) // tile, (w + tile - 1) // tile
+    pad = np.zeros((ty * tile, tx * tile, 4))
+    pad[:h, :w] = frame
+    return pad.reshape(ty, tile, tx, tile, 4).sum(axis=(1, 3))       # (ty, tx, 4)
+
+
+def _z(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    se = np.sqrt(a.var(axis=0, ddof=1) / len(a) + b.var(axis=0, ddof=1) / len(b))
+    diff = a.mean(axis=0) - b.mean(axis=0)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        z = np.where(se > 0, diff / np.where(se > 0, se, 1), np.where(diff == 0, 0.0, np.inf))
+    return z
+
+
+def compare(per_sample, tile_stream, report=None):
+    fa = [f for f, _, _ in per_sample]
+    fb = [f for f, _, _ in tile_stream]
+    tot_a = [[f[..., :3].sum(), f[..., 3].sum()] for f in fa]
+    tot_b = [[f[..., :3].sum(), f[..., 3].sum()] for f in fb]
+    z_tot = _z(tot_a, tot_b)
+    z_tile = _z([_tile_sums(f)[..., :3].sum(axis=-1) for f in fa], [_tile_sums(f)[..., :3].sum(axis=-1) for f in fb])
+    z_rays = _z([[c, s] for _, c, s in per_sample], [[c, s] for _, c, s in tile_stream])
+    if report is not None:
+        report.update({"z_sum_rgb": float(z_tot[0]), "z_sum_w": float(z_tot[1]),
+                       "max_abs_z_tile_rgb": float(np.abs(z_tile).max()), "tiles": int(z_tile.size),
+                       "z_closest_per_sample": float(z_rays[0]), "z_shadow_per_sample": float(z_rays[1]),
+                       "mean_sum_rgb": [float(np.mean([t[0] for t in tot_a])), float(np.mean([t[0] for t in tot_b]))]})
+    assert np.all(np.abs(z_tot) <= K), z_tot
+    assert np.all(np.abs(z_tile) <= K), np.abs(z_tile).max()
+    assert np.all(np.abs(z_rays) <= K), z_rays
+
+
+def test_per_sample_vs_tile_stream_oracle(rt):
+    """CPU: the oracle's per-sample RNG (the GPU's scheme) against its tile-stream RNG (the
+    reference's), C1 at 192x192, 16 spp, depth 4."""
+    scene, cam, st, fc, post = rt.load_preset("c1", 192, 192)
+    desc = scene.desc()
+    a = _frames(lambda t: ob.render(desc, cam, st, fc, 192, 192, rng_mode=0, threads=8, total_frame_index=t))
+    b = _frames(lambda t: ob.render(desc, cam, st, fc, 192, 192, rng_mode=1, threads=8, total_frame_index=t))
+    compare(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("preset,w,h,spp", [("c1", 512, 512, 16), ("c3", 192, 108, 256), ("c4", 192, 108, 256)])
+def test_gpu_vs_reference_tile_stream(rt, preset, w, h, spp):
+    """GPU frames (per-sample RNG) against the oracle's reference-stream frames."""
+    from test_gpu_parity import REPORT
+    scene, cam, st, fc, post = rt.load_preset(preset, w, h)
+    st.samples_per_pixel = spp
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        a = _frames(lambda t: dev.render(cam, st, fc, w, h, total_frame_index=t))
+    finally:
+        dev.close()
+    b = _frames(lambda t: ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=1, threads=16, total_frame_index=t))
+    rep = {}
+    try:
+        compare(a, b, rep)
+    finally:
+        REPORT[f"rng_stream_{preset}_{w}x{h}_{spp}spp"] = rep

@@ -53,9 +53,10 @@ def main():
     val, disp, dur = load(a.tag_dir)
     lines = [f"# PMC summary: {a.tag_dir}", "",
              "Per kernel, summed over dispatches (each pass is a separate bench run; dispatch counts per pass are equal).",
-             "", "| kernel | dispatches/pass | mean us | VALU util | wait (s_waitcnt) | issue-stall | VMEM lat (cyc) |"
-             " L2 hit | L1->L2 req/access | HBM rd MB/launch | HBM wr MB/launch |",
-             "|---|---|---|---|---|---|---|---|---|---|---|"]
+             "", "| kernel | dispatches/pass | mean us | waves/launch | VALU util | wait (s_waitcnt) | issue-stall |"
+             " VALU inst/wave | SALU inst/wave | VMEM inst/wave | VMEM level/inst | LDS bank-conflict | L2 hit |"
+             " L1->L2 req/access | clock GHz | HBM rd MB/launch | HBM wr MB/launch |",
+             "|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|---|"]
     out = {}
     npass = max(1, len(glob.glob(os.path.join(a.tag_dir, "pass*", ""))))
     for k in KERNELS:
@@ -68,19 +69,37 @@ def main():
         valu = g("SQ_ACTIVE_INST_VALU") / wc if wc else float("nan")
         wait = g("SQ_WAIT_ANY") / wc if wc else float("nan")
         stall = g("SQ_WAIT_INST_ANY") / wc if wc else float("nan")
-        lat = g("SQ_ACCUM_PREV_HIRES") / g("SQ_INSTS_VMEM") if g("SQ_INSTS_VMEM") else float("nan")
+        waves = g("SQ_WAVES")
+        per_wave = lambda c: g(c) / waves if waves else float("nan")
+        # SQ_INST_LEVEL_VMEM accumulates the VMEM instructions in flight per (quad-)cycle, so its ratio
+        # to SQ_INSTS_VMEM is a Little's-law latency in those units (uncalibrated on gfx950; compare
+        # kernels, not absolutes).  SQ_ACCUM_PREV_HIRES reads 0 on gfx950 / ROCm 7.2.
+        lat = g("SQ_INST_LEVEL_VMEM") / g("SQ_INSTS_VMEM") if g("SQ_INSTS_VMEM") else float("nan")
+        ldsc = g("SQ_LDS_BANK_CONFLICT") / g("SQ_LDS_IDX_ACTIVE") if g("SQ_LDS_IDX_ACTIVE") else float("nan")
         hit = g("TCC_HIT_sum") / (g("TCC_HIT_sum") + g("TCC_MISS_sum")) if g("TCC_HIT_sum") == g("TCC_HIT_sum") else float("nan")
         l1 = g("TCP_TCC_READ_REQ_sum") / g("TCP_TOTAL_CACHE_ACCESSES_sum") if g("TCP_TOTAL_CACHE_ACCESSES_sum") else float("nan")
         rd = 2.0 * g("FETCH_SIZE") * 1024 / n / 1e6
         wr = g("WRITE_SIZE") * 1024 / n / 1e6
         mean_us = sum(dur[k].values()) / max(1, len(dur[k]))
-        out[k] = {"dispatches": n, "mean_us": mean_us, "valu_util": valu, "wait_frac": wait, "issue_stall_frac": stall,
-                  "vmem_latency_cycles": lat, "l2_hit": hit, "l1_miss_req_per_access": l1,
+        # effective clock: GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS)
+        clk = g("GRBM_GUI_ACTIVE") / 8.0 / n / (mean_us * 1e3) if mean_us and n else float("nan")
+        out[k] = {"dispatches": n, "mean_us": mean_us, "waves_per_launch": waves / n if n else float("nan"),
+                  "valu_util": valu, "wait_frac": wait, "issue_stall_frac": stall,
+                  "valu_inst_per_wave": per_wave("SQ_INSTS_VALU"), "salu_inst_per_wave": per_wave("SQ_INSTS_SALU"),
+                  "vmem_inst_per_wave": per_wave("SQ_INSTS_VMEM"), "vmem_level_per_inst": lat,
+                  "lds_bank_conflict_frac": ldsc, "clock_ghz": clk, "l2_hit": hit, "l1_miss_req_per_access": l1,
                   "hbm_read_mb_per_launch": rd, "hbm_write_mb_per_launch": wr}
-        lines.append(f"| {LABEL.get(k, k)} | {n:.0f} | {mean_us:.1f} | {valu:.3f} | {wait:.3f} | {stall:.3f} | {lat:.0f} | "
-                     f"{hit:.3f} | {l1:.3f} | {rd:.1f} | {wr:.1f} |")
+        e = out[k]
+        lines.append(f"| {LABEL.get(k, k)} | {n:.0f} | {mean_us:.1f} | {e['waves_per_launch']:.0f} | {valu:.3f} | {wait:.3f} | "
+                     f"{stall:.3f} | {e['valu_inst_per_wave']:.0f} | {e['salu_inst_per_wave']:.0f} | "
+                     f"{e['vmem_inst_per_wave']:.1f} | {lat:.1f} | {ldsc:.4f} | {hit:.3f} | {l1:.3f} | {clk:.2f} | "
+                     f"{rd:.1f} | {wr:.1f} |")
     lines += ["", "VALU util = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (per wave); wait = SQ_WAIT_ANY / SQ_WAVE_CYCLES;",
-              "issue-stall = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES; VMEM latency = SQ_ACCUM_PREV_HIRES / SQ_INSTS_VMEM;",
+              "issue-stall = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES; inst/wave = SQ_INSTS_* / SQ_WAVES;",
+              "VMEM level/inst = SQ_INST_LEVEL_VMEM / SQ_INSTS_VMEM (Little's-law latency, uncalibrated units);",
+              "LDS bank-conflict = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE; L2 hit = TCC_HIT / (TCC_HIT + TCC_MISS);",
+              "L1->L2 = TCP_TCC_READ_REQ / TCP_TOTAL_CACHE_ACCESSES; clock = GRBM_GUI_ACTIVE / 8 / duration;",
+              "kernels run serialized under --pmc, so durations are isolated launch times.",
               "HBM rd = 2 x FETCH_SIZE (gfx950 correction), wr = WRITE_SIZE, per launch."]
     text = "\n".join(lines) + "\n"
     print(text)
