@@ -45,3 +45,17 @@ def rt():
 def oracle():
     import oracle_binding
     return oracle_binding.load()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _parity_report():
+    """Write the GPU tests' measured parity figures to gpurun_out/parity_report.json."""
+    yield
+    from parity_report import REPORT
+    if not REPORT:
+        return
+    import json
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    with open(os.path.join(out, "parity_report.json"), "w") as f:
+        json.dump(REPORT, f, indent=1)

@@ -18,7 +18,8 @@ import numpy as np
 import pytest
 
 import oracle_binding as ob
-from test_gpu_parity import REPORT, rel_l2, _sample_list
+from parity_report import REPORT
+from test_gpu_parity import rel_l2, _sample_list
 
 pytestmark = pytest.mark.gpu
 

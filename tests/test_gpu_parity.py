@@ -16,19 +16,7 @@ import oracle_binding as ob
 
 pytestmark = pytest.mark.gpu
 
-REPORT = {}
-
-
-@pytest.fixture(scope="module", autouse=True)
-def _parity_report():
-    """Write the measured parity figures to gpurun_out/parity_report.json (cited in DESIGN.md)."""
-    yield
-    import json
-    import os
-    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
-    os.makedirs(out, exist_ok=True)
-    with open(os.path.join(out, "parity_report.json"), "w") as f:
-        json.dump(REPORT, f, indent=1)
+from parity_report import REPORT      # noqa: E402  (written to gpurun_out/parity_report.json at session end)
 
 
 def rel_l2(a, b):

@@ -83,7 +83,7 @@ def test_per_sample_vs_tile_stream_oracle(rt):
 @pytest.mark.parametrize("preset,w,h,spp", [("c1", 512, 512, 16), ("c3", 192, 108, 256), ("c4", 192, 108, 256)])
 def test_gpu_vs_reference_tile_stream(rt, preset, w, h, spp):
     """GPU frames (per-sample RNG) against the oracle's reference-stream frames."""
-    from test_gpu_parity import REPORT
+    from parity_report import REPORT
     scene, cam, st, fc, post = rt.load_preset(preset, w, h)
     st.samples_per_pixel = spp
     dev = rt.DeviceScene(scene, 0)
