@@ -2347,32 +2347,33 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         carry = 0;
     }
     __syncthreads();
-    // exclusive scan, BK_THREADS*4 blocks per pass
-    for (uint32_t base = 0; base < nblocks; base += BK_THREADS*4) {
-        uint32_t v[4], sum = 0;
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t i = base + t*4 + k;
-            v[k] = i < nblocks ? pool.free_n[i] : 0u;
-            sum += v[k];
-        }
-        sc[t] = sum;
-        __syncthreads();
-        for (uint32_t off = 1; off < BK_THREADS; off <<= 1) {       // inclusive Hillis-Steele
-            const uint32_t add = t >= off ? sc[t - off] : 0u;
-            __syncthreads();
-            sc[t] += add;
-            __syncthreads();
-        }
-        uint32_t run = carry + sc[t] - sum;
-        for (int k = 0; k < 4; ++k) {
-            const uint32_t i = base + t*4 + k;
-            if (i < nblocks) pool.claim_base[i] = run;
-            run += v[k];
-        }
-        __syncthreads();
-        if (t == BK_THREADS - 1) carry += sc[t];
-        __syncthreads();
+    // exclusive scan of free_n: thread t owns the contiguous entries [t*E, t*E + E), sums them
+    // (all loads in flight), then a wave scan by shuffles and one barrier for the 16 wave totals.
+    // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
+    // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
+    const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
+    const uint32_t lo = t*E, hi = min(lo + E, nblocks);
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; ++i) sum += pool.free_n[i];
+    const uint32_t lane = t & 63u, wave = t >> 6;
+    uint32_t incl = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t u = __shfl_up(incl, off);
+        if (lane >= (uint32_t)off) incl += u;
     }
+    if (lane == 63) sc[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += sc[w];
+    uint32_t run = before + incl - sum;
+    for (uint32_t i = lo; i < hi; ++i) {
+        const uint32_t v = pool.free_n[i];
+        pool.claim_base[i] = run;
+        run += v;
+    }
+    if (t == BK_THREADS - 1) carry = run;
+    __syncthreads();
     if (t == 0) cnt->gen_free = carry;
 }
 

@@ -3,8 +3,8 @@
 
 usage: tools/timeline.py gpurun_out/prof_<TAG>/run_kernel_trace.csv [--bucket-ms 5]
 
-Takes the frame between the first two k_resolve launches (the bench's second frame),
-prints the mean number of kernels in flight per bucket and where the resolve starts.
+Takes the bench's second frame (frames start with k_pixel_map), prints the mean number of
+kernels in flight per bucket, the time per kernel, and where the last resolve runs.
 """
 import argparse
 import csv
@@ -16,10 +16,10 @@ def main():
     ap.add_argument("--bucket-ms", type=float, default=5.0)
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace)) if r["Kernel_Name"].startswith(("k_", "void k_"))]
-    ri = [i for i, r in enumerate(rows) if "k_resolve" in r["Kernel_Name"]]
+    ri = [i for i, r in enumerate(rows) if "k_pixel_map" in r["Kernel_Name"]]
     if len(ri) < 2:
-        raise SystemExit("need two frames (two k_resolve launches) in the trace")
-    fr = rows[ri[0] + 1:ri[1] + 1]
+        raise SystemExit("need two frames (two k_pixel_map launches) in the trace")
+    fr = rows[ri[1]:ri[2]] if len(ri) > 2 else rows[ri[0]:ri[1]]
     t0 = min(int(r["Start_Timestamp"]) for r in fr)
     t1 = max(int(r["End_Timestamp"]) for r in fr)
     bucket = int(a.bucket_ms * 1e6)
@@ -33,9 +33,19 @@ def main():
             s, b = be, b + 1
     print(f"frame {(t1 - t0) / 1e6:.1f} ms; kernels in flight per {a.bucket_ms:g} ms:")
     print(" ".join(f"{x / bucket:.1f}" for x in busy))
-    res = next(r for r in fr if "k_resolve" in r["Kernel_Name"])
-    print(f"resolve {(int(res['Start_Timestamp']) - t0) / 1e6:.1f} -> {(int(res['End_Timestamp']) - t0) / 1e6:.1f} ms")
-
+    per = {}
+    for r in fr:
+        n = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        n = n.split("<")[0] + ("<" + n.split("<")[1].split(",")[0] + ">" if "k_trace" in n else "")
+        d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        c, tot = per.get(n, (0, 0.0))
+        per[n] = (c + 1, tot + d)
+    for n, (c, tot) in sorted(per.items(), key=lambda x: -x[1][1]):
+        print(f"  {n:28s} {c:5d} launches {tot:8.1f} ms ({tot / c * 1e3:8.1f} us each)")
+    res = [r for r in fr if "k_resolve" in r["Kernel_Name"]]
+    if res:
+        r = res[-1]
+        print(f"last resolve {(int(r['Start_Timestamp']) - t0) / 1e6:.1f} -> {(int(r['End_Timestamp']) - t0) / 1e6:.1f} ms")
 
 if __name__ == "__main__":
     main()
