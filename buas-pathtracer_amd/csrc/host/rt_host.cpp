@@ -663,6 +663,46 @@ uint32_t rth_add_mesh(rth_scene* s, uint32_t mat, uint32_t mesh_id, const rt_m4x
     return id;
 }
 
+// The BVH builder the scene model uses: the host restatement, or (rth_set_bvh_device) the
+// device builder rt_build_bvh for the methods it has (midpoint, binned SAH), bit-identical.
+static int g_bvh_device = -1;
+void rth_set_bvh_device(int device) { g_bvh_device = device; }
+
+static int build_entries(std::vector<SortEntry>& in, int method, std::vector<rt_bvh_node>& nodes) {
+    if (g_bvh_device >= 0 && in.size() > 0 && (method == RTH_BVH_MIDPOINT_SPLIT || method == RTH_BVH_SAH_BINNED)) {
+        const size_t n = in.size();
+        std::vector<rt_v3> p(n), r(n);
+        for (size_t i = 0; i < n; ++i) { p[i] = rv(in[i].p); r[i] = rv(in[i].r); }
+        nodes.assign(2*n + 2, rt_bvh_node{});
+        std::vector<uint32_t> order(n);
+        uint32_t count = 0;
+        const int err = rt_build_bvh(g_bvh_device, (uint32_t)n, p.data(), r.data(),
+                                     method == RTH_BVH_MIDPOINT_SPLIT ? RT_BVH_BUILD_MIDPOINT : RT_BVH_BUILD_SAH_BINNED,
+                                     nodes.data(), &count, order.data());
+        if (err) { set_err(std::string("rt_build_bvh: ") + rt_build_bvh_last_error()); return err; }
+        nodes.resize(count);
+        std::vector<SortEntry> out(n);
+        for (size_t i = 0; i < n; ++i) out[i] = in[order[i]];
+        in.swap(out);
+        return 0;
+    }
+    nodes = build_bvh(in, method);
+    return 0;
+}
+
+int rth_build_bvh_entries(uint32_t n, const rt_v3* p, const rt_v3* r, int32_t method, rt_bvh_node* out_nodes,
+                          uint32_t* out_node_count, uint32_t* out_order) {
+    std::vector<SortEntry> in(n);
+    for (uint32_t i = 0; i < n; ++i) { in[i].index = i; in[i].p = vr(p[i]); in[i].r = vr(r[i]); }
+    std::vector<rt_bvh_node> nodes;
+    const int err = build_entries(in, method, nodes);
+    if (err) return err;
+    memcpy(out_nodes, nodes.data(), nodes.size()*sizeof(rt_bvh_node));
+    *out_node_count = (uint32_t)nodes.size();
+    for (uint32_t i = 0; i < n; ++i) out_order[i] = in[i].index;
+    return 0;
+}
+
 // create_bvh_for_mesh (RT/bvh.cpp:342-391, BVHStorage_Scalar)
 uint32_t rth_create_mesh(rth_scene* s, uint32_t n, const rt_v3* tris, const rt_v3* normals, int32_t method) {
     std::vector<SortEntry> in(n);
@@ -674,7 +714,7 @@ uint32_t rth_create_mesh(rth_scene* s, uint32_t n, const rt_v3* tris, const rt_v
         in[i].r = 0.5f*(mx - mn);
     }
     Mesh m;
-    m.nodes = build_bvh(in, method);
+    if (build_entries(in, method, m.nodes)) return 0xFFFFFFFFu;
     m.indices.resize(n);
     m.tris.resize(3*(size_t)n);
     for (uint32_t i = 0; i < n; ++i) {
@@ -775,7 +815,7 @@ int rth_create_scene_bvh(rth_scene* s) {                                      //
         e.r = 0.5f*(b.max - b.min);
         in.push_back(e);
     }
-    s->bvh_nodes = build_bvh(in, RTH_BVH_SAH_BINNED);
+    if (build_entries(in, RTH_BVH_SAH_BINNED, s->bvh_nodes)) return 0;
     s->bvh_indices.resize(in.size());
     for (size_t i = 0; i < in.size(); ++i) s->bvh_indices[i] = in[i].index;
     return 1;

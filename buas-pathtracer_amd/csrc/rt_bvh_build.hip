@@ -1,0 +1,415 @@
+// rt_bvh_build.hip — the reference's top-down BVH builders on the device.
+//
+// RT/bvh.cpp builds a BVH2 top-down, recursively: compute_bv (:6-17) over the node's entries,
+// a leaf at <= MIN_PRIMITIVES_PER_BVH_LEAF (4) entries (:236), else a split -- the midpoint of
+// the node box's largest axis (partition_midpoint :53-61) or Wald's 16-bin SAH over the
+// centroid box (partition_sah_binned :138-213) -- applied by the two-pointer swap partition
+// (partition_objects :26-51); the children pair is allocated before the left child's subtree
+// is built (construct_top_down_bvh_internal :222-287), node 1 is padding (:302-303).
+//
+// Here the recursion runs breadth first, one launch per tree level and one workgroup per node
+// of the level, and produces the SAME bits as that recursion (and as rt_host.cpp's restatement
+// of it): the nodes in the reference's numbering and the entries in the reference's order.
+//   * Box reductions: MathLib's min/max (a < b ? a : b) keep the LATER entry of two equal
+//     values, which matters only for +0 / -0; the device reduces (value, position) keys that
+//     break ties towards the later position, so the signed zeros come out as in the sequential
+//     loop.  Bin boxes likewise (LDS 64-bit atomics).
+//   * The SAH sweep over the 16 bins and the split choice run on one thread, with the host's
+//     expression order (-ffp-contract=off, IEEE division).
+//   * The partition: with A = the positions where the left scan stops (p >= split, ascending)
+//     and B = those where the right scan stops (p <= split, descending), the swaps are exactly
+//     the pairs (A[k], B[k]) for k < K, K = the number of k with A[k] < B[k] (a prefix), and
+//     the split index is min(A[K], B[K-1], n - 1).  Scans build A and B, one thread finds K by
+//     bisection, the swaps run in parallel (no position is in two pairs).
+//   * Numbering: the recursion hands out children pairs in the pre-order of the interior
+//     nodes, so a node's pair is 2 + 2 x (its pre-order rank among interior nodes); the ranks
+//     come from subtree interior counts (bottom-up pass) and a top-down pass.
+// Entries are (centre p, half extent r) of each primitive / triangle box, BVHSortEntry
+// (RT/bvh.h:25-29).  Geometry must be finite (NaN coordinates compare differently in a
+// parallel reduction than in the sequential loop).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <string>
+#include <vector>
+#include <cfloat>
+
+#include "rt_abi.h"
+
+namespace {
+thread_local std::string g_bvh_error;
+}
+
+#define BVH_OK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { g_bvh_error = std::string(#x) + ": " + hipGetErrorString(e_); err = RT_ERROR_DEVICE; goto done; } } while (0)
+
+namespace {
+
+constexpr int BT = 256;            // threads per node workgroup
+constexpr int BINS = 16;           // partition_sah_binned's bin count (RT/bvh.cpp:140)
+constexpr float BVH_EPSILON = 0.001f;   // RT/common.h:35
+
+struct BNode {                     // one node of the breadth-first build (48 B)
+    float bp[3], br[3];            // bv_p, bv_r (RT/bvh.h:31-37)
+    uint32_t first, count;         // the node's entry range
+    uint32_t axis;                 // split axis (interior)
+    uint32_t left;                 // build index of the children pair (interior), 0xFFFFFFFF: leaf
+    uint32_t icount;               // interior nodes in the subtree (numbering)
+    uint32_t fidx;                 // the node's index in the reference's numbering
+};
+
+// Ordered keys: unsigned order = float order, +0 and -0 equal (MathLib's comparisons).
+__device__ inline uint32_t ord_key(float f) {
+    uint32_t u = __float_as_uint(f);
+    if (f == 0.0f) u = 0u;
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+// min over (value, position): ties go to the larger position; max: likewise
+__device__ inline unsigned long long kmin(float v, uint32_t pos) { return ((unsigned long long)ord_key(v) << 32) | (0xFFFFFFFFu - pos); }
+__device__ inline unsigned long long kmax(float v, uint32_t pos) { return ((unsigned long long)ord_key(v) << 32) | pos; }
+__device__ inline uint32_t kmin_pos(unsigned long long k) { return 0xFFFFFFFFu - (uint32_t)k; }
+__device__ inline uint32_t kmax_pos(unsigned long long k) { return (uint32_t)k; }
+constexpr unsigned long long KMIN_NONE = ~0ull, KMAX_NONE = 0ull;
+
+__device__ inline float fmin_(float a, float b) { return a < b ? a : b; }     // MathLib min / max
+__device__ inline float fmax_(float a, float b) { return a > b ? a : b; }
+
+struct Box { float mn[3], mx[3]; };
+__device__ inline Box inverted() { Box b; for (int k = 0; k < 3; ++k) { b.mn[k] = FLT_MAX; b.mx[k] = -FLT_MAX; } return b; }
+__device__ inline Box union_of(const Box& a, const Box& b) {
+    Box r;
+    for (int k = 0; k < 3; ++k) { r.mn[k] = fmin_(a.mn[k], b.mn[k]); r.mx[k] = fmax_(a.mx[k], b.mx[k]); }
+    return r;
+}
+__device__ inline float surface_area(const Box& a) {                    // MathLib/my_math.h:1131-1138
+    const float dx = a.mx[0] - a.mn[0], dy = a.mx[1] - a.mn[1], dz = a.mx[2] - a.mn[2];
+    return 2.0f*(dx*dy + dx*dz + dy*dz);
+}
+__device__ inline uint32_t largest_axis(const Box& a) {                 // :1113-1129
+    const float d[3] = {a.mx[0] - a.mn[0], a.mx[1] - a.mn[1], a.mx[2] - a.mn[2]};
+    uint32_t ax = 0; float m = d[0];
+    if (m < d[1]) { m = d[1]; ax = 1; }
+    if (m < d[2]) { m = d[2]; ax = 2; }
+    return ax;
+}
+
+__device__ inline float comp(const float4& v, uint32_t a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+__device__ unsigned long long wave_min64(unsigned long long v) {
+    for (int m = 32; m; m >>= 1) { const unsigned long long o = __shfl_xor(v, m); v = o < v ? o : v; }
+    return v;
+}
+__device__ unsigned long long wave_max64(unsigned long long v) {
+    for (int m = 32; m; m >>= 1) { const unsigned long long o = __shfl_xor(v, m); v = o > v ? o : v; }
+    return v;
+}
+
+// Exclusive rank of `pred` among the block's threads, and the block total.  All threads call it.
+__device__ uint32_t block_rank(bool pred, uint32_t* sc, uint32_t* total) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(pred);
+    if (lane == 0) sc[wave] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, all = 0;
+    for (uint32_t w = 0; w < BT / 64; ++w) { const uint32_t c = sc[w]; if (w < wave) before += c; all += c; }
+    __syncthreads();
+    *total = all;
+    return before + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+// One tree level: workgroup b builds node lo + b (its box, its split, the partition of its
+// entries) and appends its children pair to the node array.
+__global__ void __launch_bounds__(BT) k_bvh_level(float4* ep, float4* er, BNode* nodes, uint32_t lo, uint32_t* counter,
+                                                  int method, uint32_t* sA, uint32_t* sB) {
+    __shared__ unsigned long long red[BT / 64][12];
+    __shared__ unsigned long long bmin[BINS][3], bmax[BINS][3];
+    __shared__ uint32_t bcnt[BINS];
+    __shared__ uint32_t sc[BT / 64];
+    __shared__ float s_split;
+    __shared__ uint32_t s_axis, s_do, s_K, s_na, s_nb;
+    const uint32_t id = lo + blockIdx.x;
+    const uint32_t first = nodes[id].first, n = nodes[id].count;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    // compute_bv (RT/bvh.cpp:6-17): bv = union of the entry boxes, cr = the centroid box
+    unsigned long long k[12];
+    for (int j = 0; j < 6; ++j) { k[j] = KMIN_NONE; k[6 + j] = KMAX_NONE; }
+    for (uint32_t i = tid; i < n; i += BT) {
+        const float4 p = ep[first + i], r = er[first + i];
+        const float lo3[3] = {p.x - r.x, p.y - r.y, p.z - r.z}, hi3[3] = {p.x + r.x, p.y + r.y, p.z + r.z};
+        const float pc[3] = {p.x, p.y, p.z};
+        for (int a = 0; a < 3; ++a) {
+            unsigned long long t;
+            t = kmin(lo3[a], i); k[a] = t < k[a] ? t : k[a];
+            t = kmin(pc[a], i);  k[3 + a] = t < k[3 + a] ? t : k[3 + a];
+            t = kmax(hi3[a], i); k[6 + a] = t > k[6 + a] ? t : k[6 + a];
+            t = kmax(pc[a], i);  k[9 + a] = t > k[9 + a] ? t : k[9 + a];
+        }
+    }
+    for (int j = 0; j < 6; ++j) { k[j] = wave_min64(k[j]); k[6 + j] = wave_max64(k[6 + j]); }
+    if (lane == 0) for (int j = 0; j < 12; ++j) red[wave][j] = k[j];
+    __syncthreads();
+    Box bv = inverted(), cr = inverted();
+    unsigned long long K12[12];
+    for (int j = 0; j < 6; ++j) {
+        unsigned long long a = red[0][j], b = red[0][6 + j];
+        for (uint32_t w = 1; w < BT / 64; ++w) {
+            a = red[w][j] < a ? red[w][j] : a;
+            b = red[w][6 + j] > b ? red[w][6 + j] : b;
+        }
+        K12[j] = a; K12[6 + j] = b;
+    }
+    if (n) {
+        for (int a = 0; a < 3; ++a) {            // the winning entries' values, bit for bit (signed zeros)
+            const uint32_t i0 = kmin_pos(K12[a]), i1 = kmin_pos(K12[3 + a]), i2 = kmax_pos(K12[6 + a]), i3 = kmax_pos(K12[9 + a]);
+            bv.mn[a] = comp(ep[first + i0], a) - comp(er[first + i0], a);
+            cr.mn[a] = comp(ep[first + i1], a);
+            bv.mx[a] = comp(ep[first + i2], a) + comp(er[first + i2], a);
+            cr.mx[a] = comp(ep[first + i3], a);
+        }
+    }
+    if (tid == 0) {
+        for (int a = 0; a < 3; ++a) {
+            nodes[id].bp[a] = 0.5f*(bv.mn[a] + bv.mx[a]);
+            nodes[id].br[a] = 0.5f*(bv.mx[a] - bv.mn[a]);
+        }
+        nodes[id].left = 0xFFFFFFFFu;
+        nodes[id].axis = 0;
+    }
+    if (n <= 4) return;                          // MIN_PRIMITIVES_PER_BVH_LEAF (RT/bvh.h:23, bvh.cpp:236)
+    // ---- the split
+    if (method == RT_BVH_BUILD_MIDPOINT) {       // partition_midpoint (:53-61)
+        if (tid == 0) {
+            const uint32_t ax = largest_axis(bv);
+            s_axis = ax;
+            s_split = 0.5f*(bv.mn[ax] + bv.mx[ax]);
+            s_do = 1;
+        }
+    } else {                                     // partition_sah_binned (:138-213)
+        const uint32_t axis = largest_axis(cr);
+        const float k0 = cr.mn[axis];
+        const float k1 = ((float)BINS*(1.0f - BVH_EPSILON)) / (cr.mx[axis] - cr.mn[axis]);
+        for (int b = tid; b < BINS; b += BT) {
+            bcnt[b] = 0;
+            for (int a = 0; a < 3; ++a) { bmin[b][a] = KMIN_NONE; bmax[b][a] = KMAX_NONE; }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < n; i += BT) {
+            const float4 p = ep[first + i], r = er[first + i];
+            const float f = k1*(comp(p, axis) - k0);
+            uint32_t bi = (f == f && f > 0.0f) ? (uint32_t)f : 0u;        // (u32)NaN -> 0 as on x64
+            if (bi >= (uint32_t)BINS) bi = BINS - 1;
+            atomicAdd(&bcnt[bi], 1u);
+            atomicMin(&bmin[bi][0], kmin(p.x - r.x, i)); atomicMin(&bmin[bi][1], kmin(p.y - r.y, i));
+            atomicMin(&bmin[bi][2], kmin(p.z - r.z, i));
+            atomicMax(&bmax[bi][0], kmax(p.x + r.x, i)); atomicMax(&bmax[bi][1], kmax(p.y + r.y, i));
+            atomicMax(&bmax[bi][2], kmax(p.z + r.z, i));
+        }
+        __syncthreads();
+        if (tid == 0) {
+            struct Bin { uint32_t count; Box b; };
+            Bin bins[BINS], ls[BINS], rs[BINS];
+            for (int b = 0; b < BINS; ++b) {
+                bins[b].count = bcnt[b];
+                bins[b].b = inverted();
+                if (bcnt[b]) {
+                    for (int a = 0; a < 3; ++a) {
+                        const uint32_t i0 = kmin_pos(bmin[b][a]), i1 = kmax_pos(bmax[b][a]);
+                        bins[b].b.mn[a] = comp(ep[first + i0], a) - comp(er[first + i0], a);
+                        bins[b].b.mx[a] = comp(ep[first + i1], a) + comp(er[first + i1], a);
+                    }
+                }
+                ls[b].count = rs[b].count = 0;
+                ls[b].b = rs[b].b = inverted();
+            }
+            const float parent = (float)n*surface_area(bv);
+            float best = parent, split_p = 0.0f;
+            Bin empty; empty.count = 0; empty.b = inverted();
+            for (int i = 0; i < BINS - 1; ++i) {
+                const Bin& prev = i > 0 ? ls[i - 1] : empty;
+                ls[i].count = prev.count + bins[i].count;
+                ls[i].b = union_of(prev.b, bins[i].b);
+            }
+            for (int i = BINS - 1; i >= 1; --i) {
+                const Bin& prev = i < BINS - 1 ? rs[i + 1] : empty;
+                rs[i].count = prev.count + bins[i].count;
+                rs[i].b = union_of(prev.b, bins[i].b);
+                const float l = (float)ls[i].count*surface_area(ls[i].b);
+                const float r = (float)rs[i].count*surface_area(rs[i].b);
+                const float s = l + r;
+                if ((s > 0.0f) && (s < best)) { best = s; split_p = k0 + ((float)i / k1); }
+            }
+            s_axis = axis;
+            s_split = split_p;
+            s_do = best < parent ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    if (!s_do) return;                           // no split beats the parent: a leaf
+    const uint32_t axis = s_axis;
+    const float split = s_split;
+    // ---- partition_objects (:26-51): the stop lists of the two scans
+    uint32_t na = 0, nb = 0;
+    for (uint32_t base = 0; base < n; base += BT) {
+        const uint32_t i = base + tid;
+        const bool in = i < n;
+        const float v = in ? comp(ep[first + i], axis) : 0.0f;
+        const bool lstop = in && !(v < split);   // the left scan stops at p >= split
+        const bool rstop = in && !(v > split);   // the right scan stops at p <= split
+        uint32_t ta, tb;
+        const uint32_t ra = block_rank(lstop, sc, &ta);
+        const uint32_t rb = block_rank(rstop, sc, &tb);
+        if (lstop) sA[first + na + ra] = i;
+        if (rstop) sB[first + nb + rb] = i;
+        na += ta; nb += tb;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        // B[k] (k-th stop of the right scan) = sB[first + nb - 1 - k]; K = #k with A[k] < B[k]
+        uint32_t lo_k = 0, hi_k = na < nb ? na : nb;
+        while (lo_k < hi_k) {
+            const uint32_t mid = (lo_k + hi_k) / 2;
+            if (sA[first + mid] < sB[first + nb - 1 - mid]) lo_k = mid + 1; else hi_k = mid;
+        }
+        s_K = lo_k; s_na = na; s_nb = nb;
+    }
+    __syncthreads();
+    const uint32_t K = s_K;
+    for (uint32_t kk = tid; kk < K; kk += BT) {
+        const uint32_t a = first + sA[first + kk], b = first + sB[first + nb - 1 - kk];
+        const float4 pa = ep[a], ra = er[a], pb = ep[b], rb = er[b];
+        ep[a] = pb; er[a] = rb; ep[b] = pa; er[b] = ra;
+    }
+    if (tid == 0) {
+        uint32_t si = n - 1;
+        if (K < s_na) si = sA[first + K] < si ? sA[first + K] : si;
+        if (K > 0) { const uint32_t b = sB[first + s_nb - K]; si = b < si ? b : si; }
+        if (si != 0 && si <= n - 1) {            // construct (:228-237): both children non-empty
+            const uint32_t c = atomicAdd(counter, 2u);
+            nodes[id].left = c;
+            nodes[id].axis = axis;
+            nodes[c].first = first;          nodes[c].count = si;
+            nodes[c + 1].first = first + si; nodes[c + 1].count = n - si;
+        }
+    }
+}
+
+// Subtree interior counts, one level at a time from the deepest.
+__global__ void k_bvh_icount(BNode* nodes, uint32_t lo, uint32_t hi) {
+    const uint32_t id = lo + blockIdx.x*blockDim.x + threadIdx.x;
+    if (id >= hi) return;
+    const uint32_t l = nodes[id].left;
+    nodes[id].icount = l == 0xFFFFFFFFu ? 0u : 1u + nodes[l].icount + nodes[l + 1].icount;
+}
+// The reference's numbering, one level at a time from the root: a node's pair is handed out in
+// the pre-order of the interior nodes (construct: l = node_count++, r = node_count++, then the
+// left subtree).  `fidx` of the children; `icount` is reused as the pre-order rank once read.
+__global__ void k_bvh_number(BNode* nodes, const uint32_t* rank_in, uint32_t* rank_out, uint32_t lo, uint32_t hi) {
+    const uint32_t id = lo + blockIdx.x*blockDim.x + threadIdx.x;
+    if (id >= hi) return;
+    const uint32_t l = nodes[id].left;
+    if (l == 0xFFFFFFFFu) return;
+    const uint32_t q = rank_in[id];                      // this interior node's pre-order rank
+    nodes[l].fidx = 2u + 2u*q;
+    nodes[l + 1].fidx = 3u + 2u*q;
+    rank_out[l] = q + 1u;                                // left child first in pre-order
+    rank_out[l + 1] = q + 1u + nodes[l].icount;          // then the left subtree's interior nodes
+}
+__global__ void k_bvh_emit(const BNode* nodes, uint32_t count, rt_bvh_node* out) {
+    const uint32_t id = blockIdx.x*blockDim.x + threadIdx.x;
+    if (id >= count) return;
+    const BNode nd = nodes[id];
+    rt_bvh_node o;
+    o.bv_p = {nd.bp[0], nd.bp[1], nd.bp[2]};
+    o.bv_r = {nd.br[0], nd.br[1], nd.br[2]};
+    if (nd.left == 0xFFFFFFFFu) { o.left_first = nd.first; o.count = (uint16_t)nd.count; o.split_axis = 0; }
+    else { o.left_first = nodes[nd.left].fidx; o.count = 0; o.split_axis = (uint16_t)nd.axis; }
+    out[nd.fidx] = o;
+}
+__global__ void k_bvh_order(const float4* ep, uint32_t n, uint32_t* order) {
+    const uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
+    if (i < n) order[i] = __float_as_uint(ep[i].w);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_build_bvh_last_error(void) { return g_bvh_error.c_str(); }
+
+int rt_build_bvh(int device, uint32_t n, const rt_v3* p, const rt_v3* r, int method, rt_bvh_node* out_nodes,
+                 uint32_t* out_node_count, uint32_t* out_order) {
+    if (!p || !r || !out_nodes || !out_node_count || !out_order || n == 0) { g_bvh_error = "null argument or no entries"; return RT_ERROR_INVALID; }
+    if (method != RT_BVH_BUILD_MIDPOINT && method != RT_BVH_BUILD_SAH_BINNED) { g_bvh_error = "unsupported method"; return RT_ERROR_INVALID; }
+    if (n >= 0x7FFFFFFFu / 2u) { g_bvh_error = "too many entries"; return RT_ERROR_INVALID; }
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) { g_bvh_error = "no HIP device visible"; return RT_ERROR_NO_DEVICE; }
+    if (device < 0 || device >= count) { g_bvh_error = "device index out of range"; return RT_ERROR_INVALID; }
+    int err = RT_OK;
+    const size_t cap = 2*(size_t)n + 1;
+    float4 *d_p = nullptr, *d_r = nullptr;
+    BNode* d_nodes = nullptr;
+    uint32_t *d_a = nullptr, *d_b = nullptr, *d_cnt = nullptr, *d_rank = nullptr, *d_order = nullptr;
+    rt_bvh_node* d_out = nullptr;
+    std::vector<float4> hp(n), hr(n);
+    std::vector<uint32_t> levels;               // node-array offset where each level starts
+    uint32_t interior = 0, total = 1;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t idx = i; float f; memcpy(&f, &idx, 4);
+        hp[i] = make_float4(p[i].x, p[i].y, p[i].z, f);
+        hr[i] = make_float4(r[i].x, r[i].y, r[i].z, 0.0f);
+    }
+    BVH_OK(hipSetDevice(device));
+    BVH_OK(hipMalloc(&d_p, sizeof(float4)*n));
+    BVH_OK(hipMalloc(&d_r, sizeof(float4)*n));
+    BVH_OK(hipMalloc(&d_nodes, sizeof(BNode)*cap));
+    BVH_OK(hipMalloc(&d_a, sizeof(uint32_t)*n));
+    BVH_OK(hipMalloc(&d_b, sizeof(uint32_t)*n));
+    BVH_OK(hipMalloc(&d_cnt, sizeof(uint32_t)));
+    BVH_OK(hipMalloc(&d_rank, sizeof(uint32_t)*cap));
+    BVH_OK(hipMalloc(&d_order, sizeof(uint32_t)*n));
+    BVH_OK(hipMemcpy(d_p, hp.data(), sizeof(float4)*n, hipMemcpyHostToDevice));
+    BVH_OK(hipMemcpy(d_r, hr.data(), sizeof(float4)*n, hipMemcpyHostToDevice));
+    {
+        BNode root = {};
+        root.first = 0; root.count = n; root.left = 0xFFFFFFFFu; root.fidx = 0;
+        BVH_OK(hipMemcpy(d_nodes, &root, sizeof(BNode), hipMemcpyHostToDevice));
+        BVH_OK(hipMemcpy(d_cnt, &total, sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    for (uint32_t lo = 0, hi = 1; lo < hi;) {                  // one launch per level
+        levels.push_back(lo);
+        k_bvh_level<<<hi - lo, BT>>>(d_p, d_r, d_nodes, lo, d_cnt, method, d_a, d_b);
+        BVH_OK(hipGetLastError());
+        uint32_t next = 0;
+        BVH_OK(hipMemcpy(&next, d_cnt, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        interior += (next - hi) / 2;
+        lo = hi; hi = next;
+        total = next;
+        if (levels.size() > 4096) { g_bvh_error = "BVH deeper than 4096 levels"; err = RT_ERROR_INVALID; goto done; }
+    }
+    levels.push_back(total);
+    for (size_t L = levels.size() - 1; L-- > 0;) {             // subtree interior counts, deepest level first
+        const uint32_t lo = levels[L], hi = levels[L + 1];
+        k_bvh_icount<<<(hi - lo + 255) / 256, 256>>>(d_nodes, lo, hi);
+    }
+    BVH_OK(hipMemset(d_rank, 0, sizeof(uint32_t)*cap));        // the root's pre-order rank is 0
+    for (size_t L = 0; L + 1 < levels.size(); ++L) {
+        const uint32_t lo = levels[L], hi = levels[L + 1];
+        k_bvh_number<<<(hi - lo + 255) / 256, 256>>>(d_nodes, d_rank, d_rank, lo, hi);
+    }
+    {
+        const uint32_t nodes_out = 2 + 2*interior;              // root, padding, the pairs
+        BVH_OK(hipMalloc(&d_out, sizeof(rt_bvh_node)*nodes_out));
+        BVH_OK(hipMemset(d_out, 0, sizeof(rt_bvh_node)*nodes_out));   // node 1: padding (:302-303)
+        k_bvh_emit<<<(total + 255) / 256, 256>>>(d_nodes, total, d_out);
+        k_bvh_order<<<(n + 255) / 256, 256>>>(d_p, n, d_order);
+        BVH_OK(hipGetLastError());
+        BVH_OK(hipMemcpy(out_nodes, d_out, sizeof(rt_bvh_node)*nodes_out, hipMemcpyDeviceToHost));
+        BVH_OK(hipMemcpy(out_order, d_order, sizeof(uint32_t)*n, hipMemcpyDeviceToHost));
+        *out_node_count = nodes_out;
+    }
+done:
+    (void)hipFree(d_p); (void)hipFree(d_r); (void)hipFree(d_nodes); (void)hipFree(d_a); (void)hipFree(d_b);
+    (void)hipFree(d_cnt); (void)hipFree(d_rank); (void)hipFree(d_order); (void)hipFree(d_out);
+    return err;
+}
+
+}  // extern "C"

@@ -329,6 +329,22 @@ int rt_postprocess_device(int device, const float* d_pixels, uint32_t w, uint32_
 int rt_postprocess(int device, const rt_accumulation_buffer* accum, const rt_post_settings* post,
                    uint32_t total_frame_index, uint32_t* out_bgra);
 
+/* The reference's top-down BVH builders on the device (RT/bvh.cpp:222-326 with
+ * partition_midpoint :53-61 or partition_sah_binned :138-213, the partition of :26-51):
+ * one launch per tree level, one workgroup per node.  Bit-identical to the sequential
+ * recursion: out_nodes holds the reference's BVHNode array (root 0, node 1 padding,
+ * children pairs in its order; capacity 2n + 2 nodes), out_order[i] the entry index at
+ * position i of the partitioned entry array (BVHSortEntry::index).  Entries are the
+ * centre p and half extent r of each primitive's or triangle's box (BVHSortEntry,
+ * RT/bvh.h:25-29).  Host pointers; returns an rt_status (text: rt_build_bvh_last_error). */
+enum rt_bvh_build_method {
+    RT_BVH_BUILD_MIDPOINT   = 0,    /* BVH_MidpointSplit */
+    RT_BVH_BUILD_SAH_BINNED = 1,    /* BVH_SAHBinned (16 bins) */
+};
+int rt_build_bvh(int device, uint32_t n, const rt_v3* p, const rt_v3* r, int method,
+                 rt_bvh_node* out_nodes, uint32_t* out_node_count, uint32_t* out_order);
+const char* rt_build_bvh_last_error(void);
+
 /* Record per-stage HIP-event timings into rt_stats::kernel_ms (off by default). */
 int rt_set_profiling(int enable);
 /* The same for a subset of stages: bit k = stage k of rt_kernel_stage (other stages

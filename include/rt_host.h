@@ -87,6 +87,15 @@ void     rth_set_sky(rth_scene* s, rt_v3 top, rt_v3 bot);
 /* load_environment_map: parse_hdr + luma CDF (the CDF is built, as in the reference) */
 int      rth_load_environment_map(rth_scene* s, const char* hdr_path);
 
+/* Build the BVHs of rth_create_mesh / rth_create_scene_bvh on `device` with rt_build_bvh
+ * (midpoint and binned SAH; bit-identical to the host builder); -1 (the default): on the host.
+ * rth_build_bvh_entries: the builder on raw BVHSortEntry boxes (centre p, half extent r),
+ * with the same outputs as rt_build_bvh; uses the device when one was set.  Returns an
+ * rt_status. */
+void     rth_set_bvh_device(int device);
+int      rth_build_bvh_entries(uint32_t n, const rt_v3* p, const rt_v3* r, int32_t method,
+                               rt_bvh_node* out_nodes, uint32_t* out_node_count, uint32_t* out_order);
+
 /* create_scene_bvh (binned SAH over primitives 1..n) */
 int      rth_create_scene_bvh(rth_scene* s);
 /* Flattened view, valid until the scene is modified or destroyed. */
