@@ -15,7 +15,8 @@ import glob
 import json
 import os
 
-KERNELS = ["k_generate", "k_trace<false", "k_shade", "k_trace<true", "k_splat", "k_resolve", "k_bookkeep"]
+KERNELS = ["k_generate", "k_trace<false", "k_shade", "k_trace<true", "k_splat", "k_resolve_tiles", "k_resolve",
+           "k_combine_partials", "k_bookkeep"]
 LABEL = {"k_trace<false": "k_extend (k_trace<false, .>)", "k_trace<true": "k_connect (k_trace<true, .>)"}
 KEYS = {"k_trace<false": "k_extend", "k_trace<true": "k_connect"}
 
