@@ -219,12 +219,12 @@ def main():
     elapsed = time.perf_counter() - t0
     rt.lib().rt_set_profiling(0)
 
-    totals = torch.tensor([closest, shadow, samples], dtype=torch.float64, device=f"cuda:{device}")
+    totals = torch.tensor([closest, shadow, samples, traced, traced_sh], dtype=torch.float64, device=f"cuda:{device}")
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
     if distributed:
         dist.all_reduce(totals, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    closest_all, shadow_all, samples_all = [float(x) for x in totals.tolist()]
+    closest_all, shadow_all, samples_all, traced_all, traced_sh_all = [float(x) for x in totals.tolist()]
     elapsed = float(tmax.item())
 
     if rank == 0:
@@ -316,6 +316,9 @@ def main():
             "samples_per_s_per_gpu": round(samples_all / elapsed / world, 1),
             "closest_hit_rays": int(closest_all),
             "shadow_rays": int(shadow_all),
+            # the rays handed to the BVH traversal kernels (closest, shadow); the rest were settled by the
+            # planes / top-level prologue where they were made
+            "traced_rays": [int(traced_all), int(traced_sh_all)],
             "config": {"workload": f"{args.config}: {cfg['preset']} {w}x{h} {st.samples_per_pixel}spp "
                                    f"depth {st.max_bounce_count}", "width": w, "height": h,
                        "spp": st.samples_per_pixel, "max_depth": st.max_bounce_count,
