@@ -2492,7 +2492,7 @@ struct Partition {
     Pool pool = {};
     std::vector<void*> pool_allocs;
     Counters* cnt = nullptr;
-    Counters* cnt_host = nullptr;       // pinned, [2]: the counters after chunk c land in [c % 2]
+    Counters* cnt_host = nullptr;       // pinned, [3]: the counters after chunk c land in [c % 2]; [2] stages the frame's initial counters
     hipEvent_t chunk_done[2] = {};
     uint2* spill = nullptr;             // traversal stack levels beyond STACK_LDS
     hipStream_t own_stream = nullptr;   // partitions > 0 (partition 0 runs on the caller's stream)
@@ -2524,6 +2524,20 @@ struct rt_scene {
     size_t partial_cap = 0;
     uint32_t* d_aux = nullptr;      // streaming splat: partial pointers, then k_resolve_tiles' blocks
     size_t aux_cap = 0;
+    // The frame layout of the last rt_render_device (owned tiles, pixel map, tile bases, resolve
+    // blocks): rebuilt and uploaded only when the frame size, tiling, shard or filter radius changes.
+    struct Layout {
+        bool valid = false;
+        uint32_t w = 0, h = 0, tw = 0, th = 0, si = 0, sc = 0;
+        std::vector<uint32_t> ids, prefix;
+        uint64_t owned_px = 0;
+        std::vector<int32_t> base;
+        int blocks_ks = -1;                 // radius the resolve blocks were built for (-1: none)
+        uint32_t nblocks = 0;
+        const void* aux_partials = nullptr; // d_partials / npx the device pointer table holds
+        size_t aux_npx = 0;
+        int aux_parts = -1;
+    } layout;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
 };
@@ -2690,7 +2704,7 @@ int ensure_partition(rt_scene* s, int k) {
     Partition& pt = s->part[k];
     if (pt.cnt) return RT_OK;
     HIP_OK(hipMalloc(&pt.cnt, sizeof(Counters)));
-    HIP_OK(hipHostMalloc(&pt.cnt_host, 2*sizeof(Counters)));
+    HIP_OK(hipHostMalloc(&pt.cnt_host, 3*sizeof(Counters)));
     for (auto& e : pt.chunk_done) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipMalloc(&pt.spill, sizeof(uint2)*(size_t)(STACK_DEPTH - STACK_LDS)*s->trace_grid*TB));
     if (k > 0) HIP_OK(hipStreamCreateWithFlags(&pt.own_stream, hipStreamNonBlocking));
@@ -2864,7 +2878,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             }
         }
         init.start_sample = init.next_sample;
-        HIP_OK(hipMemcpyAsync(pt.cnt, &init, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
+        pt.cnt_host[2] = init;           // pinned: the copy is asynchronous (the frame ends before the next write)
+        HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + 2, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
         k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{});
@@ -3443,45 +3458,69 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.tile_w = tiles->tile_w; fp.tile_h = tiles->tile_h;
     fp.tcx = (w + tiles->tile_w - 1) / tiles->tile_w;
     uint32_t tcy = (h + tiles->tile_h - 1) / tiles->tile_h;
-    // owned tiles: t % shard_count == shard_index, descending like the reference's queue (:555)
-    std::vector<uint32_t> ids, prefix(1, 0);
-    uint64_t owned_px = 0;
-    for (uint32_t t = fp.tcx*tcy; t-- > 0;) {
-        if (t % tiles->shard_count != tiles->shard_index) continue;
-        uint32_t min_x = tiles->tile_w*(t % fp.tcx), min_y = tiles->tile_h*(t / fp.tcx);
-        uint32_t tw = std::min(w, min_x + tiles->tile_w) - min_x, th = std::min(h, min_y + tiles->tile_h) - min_y;
-        ids.push_back(t);
-        owned_px += (uint64_t)tw*th;
-        prefix.push_back((uint32_t)std::min<uint64_t>(owned_px, 0xFFFFFFFFull));
-    }
-    if (ids.empty()) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
-    size_t need = ids.size() + prefix.size();
-    if (s->tiles_cap < need) {
-        if (s->d_tiles) (void)hipFree(s->d_tiles);
-        s->d_tiles = nullptr;
-        HIP_OK(hipMalloc(&s->d_tiles, need*sizeof(uint32_t)));
-        s->tiles_cap = need;
-    }
-    std::vector<uint32_t> packed(ids);
-    packed.insert(packed.end(), prefix.begin(), prefix.end());
-    HIP_OK(hipMemcpyAsync(s->d_tiles, packed.data(), packed.size()*sizeof(uint32_t), hipMemcpyHostToDevice, stream));
-    HIP_OK(hipMemcpyAsync(s->d_lut, filter->cache, 512*sizeof(float), hipMemcpyHostToDevice, stream));
-    fp.ntiles = (uint32_t)ids.size();
-    fp.tile_ids = s->d_tiles;
-    fp.tile_prefix = s->d_tiles + ids.size();
     if (w > 65535 || h > 65535) { set_error("frame larger than 65535 pixels a side"); return RT_ERROR_INVALID; }
-    if (owned_px >= 0x80000000ull) {        // tile_base / pixel indices are 31-bit
+    auto& L = s->layout;
+    const bool same = L.valid && L.w == w && L.h == h && L.tw == tiles->tile_w && L.th == tiles->tile_h &&
+                      L.si == tiles->shard_index && L.sc == tiles->shard_count;
+    if (!same) {
+        // owned tiles: t % shard_count == shard_index, descending like the reference's queue (:555)
+        L.valid = false;
+        L.ids.clear(); L.prefix.assign(1, 0); L.owned_px = 0;
+        for (uint32_t t = fp.tcx*tcy; t-- > 0;) {
+            if (t % tiles->shard_count != tiles->shard_index) continue;
+            uint32_t min_x = tiles->tile_w*(t % fp.tcx), min_y = tiles->tile_h*(t / fp.tcx);
+            uint32_t tw = std::min(w, min_x + tiles->tile_w) - min_x, th = std::min(h, min_y + tiles->tile_h) - min_y;
+            L.ids.push_back(t);
+            L.owned_px += (uint64_t)tw*th;
+            L.prefix.push_back((uint32_t)std::min<uint64_t>(L.owned_px, 0xFFFFFFFFull));
+        }
+    }
+    const std::vector<uint32_t>& ids = L.ids;
+    const std::vector<uint32_t>& prefix = L.prefix;
+    if (ids.empty()) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
+    if (L.owned_px >= 0x80000000ull) {      // tile_base / pixel indices are 31-bit
         set_error("shard of 2^31 or more pixels: use more shards"); return RT_ERROR_INVALID;
     }
+    fp.ntiles = (uint32_t)ids.size();
     fp.pixels = prefix.back();
-    if (s->pixmap_cap < fp.pixels) {
-        if (s->d_pixmap) (void)hipFree(s->d_pixmap);
-        s->d_pixmap = nullptr; s->pixmap_cap = 0;
-        HIP_OK(hipMalloc(&s->d_pixmap, sizeof(uint32_t)*(size_t)fp.pixels));
-        s->pixmap_cap = fp.pixels;
+    const size_t ntile_all = (size_t)fp.tcx*tcy;
+    if (!same) {
+        size_t need = ids.size() + prefix.size();
+        if (s->tiles_cap < need) {
+            if (s->d_tiles) (void)hipFree(s->d_tiles);
+            s->d_tiles = nullptr;
+            HIP_OK(hipMalloc(&s->d_tiles, need*sizeof(uint32_t)));
+            s->tiles_cap = need;
+        }
+        std::vector<uint32_t> packed(ids);
+        packed.insert(packed.end(), prefix.begin(), prefix.end());
+        HIP_OK(hipMemcpy(s->d_tiles, packed.data(), packed.size()*sizeof(uint32_t), hipMemcpyHostToDevice));
+        if (s->pixmap_cap < fp.pixels) {
+            if (s->d_pixmap) (void)hipFree(s->d_pixmap);
+            s->d_pixmap = nullptr; s->pixmap_cap = 0;
+            HIP_OK(hipMalloc(&s->d_pixmap, sizeof(uint32_t)*(size_t)fp.pixels));
+            s->pixmap_cap = fp.pixels;
+        }
+        L.base.assign(ntile_all, -1);
+        for (size_t i = 0; i < ids.size(); ++i) L.base[ids[i]] = (int32_t)prefix[i];
+        if (s->tile_base_cap < ntile_all) {
+            if (s->d_tile_base) (void)hipFree(s->d_tile_base);
+            s->d_tile_base = nullptr;
+            HIP_OK(hipMalloc(&s->d_tile_base, sizeof(int32_t)*ntile_all));
+            s->tile_base_cap = ntile_all;
+        }
+        HIP_OK(hipMemcpy(s->d_tile_base, L.base.data(), sizeof(int32_t)*ntile_all, hipMemcpyHostToDevice));
     }
-    k_pixel_map<<<fp.ntiles, 256, 0, stream>>>(fp, s->d_pixmap);
-    HIP_OK(hipGetLastError());
+    HIP_OK(hipMemcpyAsync(s->d_lut, filter->cache, 512*sizeof(float), hipMemcpyHostToDevice, stream));
+    fp.tile_ids = s->d_tiles;
+    fp.tile_prefix = s->d_tiles + ids.size();
+    if (!same) {
+        k_pixel_map<<<fp.ntiles, 256, 0, stream>>>(fp, s->d_pixmap);
+        HIP_OK(hipGetLastError());
+        L.w = w; L.h = h; L.tw = tiles->tile_w; L.th = tiles->tile_h; L.si = tiles->shard_index; L.sc = tiles->shard_count;
+        L.blocks_ks = -1;
+        L.valid = true;
+    }
     fp.pix_xy = s->d_pixmap;
     fill_camera(fp, camera);
     fp.lut = s->d_lut;
@@ -3499,40 +3538,46 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     // one pass per partition does not fit.
     const uint32_t spp = st->samples_per_pixel;
     const int ks = fp.cache_size ? fp.kernel_size : 0;
-    double budget;
-    if (const char* bud = getenv("RT_SAMPLE_BUDGET_GB")) {
-        budget = atof(bud)*1e9;
-    } else {
+    const FrameShape shape = frame_shape(total, spp);
+    int want_mode = g_splat_mode;
+    if (const char* e = getenv("RT_SPLAT")) want_mode = atoi(e);
+    // the splat for a record budget (bytes): the mode, and for STREAM the ring and chunk
+    auto plan_splat = [&](double budget, SplatCfg& sp, size_t& need_rec) {
+        sp = SplatCfg{};
+        sp.passes = spp;
+        sp.mode = want_mode;
+        need_rec = 0;
+        if (sp.mode == RT_SPLAT_EXACT && (double)total*20.0 > budget) sp.mode = RT_SPLAT_STREAM;
+        if (sp.mode == RT_SPLAT_STREAM && ks > 12) sp.mode = (double)total*20.0 <= budget ? RT_SPLAT_EXACT : RT_SPLAT_ATOMIC;
+        if (sp.mode == RT_SPLAT_STREAM) {
+            // a resolve every ~32M samples; the ring holds the passes not yet resolved: the chunk,
+            // the claims of the iterations a path can live (about 5 pool fills) and slack
+            const uint32_t per_part = (spp + shape.nparts - 1) / shape.nparts;
+            sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull), per_part);
+            if (const char* e = getenv("RT_SPLAT_CHUNK")) sp.chunk = std::max(1, atoi(e));
+            const unsigned long long lag = (5ull*shape.pool_n + fp.pixels - 1) / fp.pixels;
+            sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, per_part);
+            if (const char* e = getenv("RT_SPLAT_RING")) sp.ring = std::max(1, atoi(e));
+            sp.chunk = std::min(sp.chunk, sp.ring);                   // the planner needs chunk <= ring
+            while (sp.ring > 1 && 20.0*(double)shape.nparts*sp.ring*fp.pixels > budget) {
+                sp.ring = std::max(1u, sp.ring / 2);
+                sp.chunk = std::min(sp.chunk, sp.ring);
+            }
+            need_rec = (size_t)shape.nparts*sp.ring*fp.pixels;
+            if (20.0*(double)need_rec > budget) { sp.mode = RT_SPLAT_ATOMIC; need_rec = 0; }
+        }
+        if (sp.mode == RT_SPLAT_EXACT) need_rec = (size_t)total;
+    };
+    // The records held already need no budget: the free-memory query runs only when they must grow.
+    SplatCfg sp;
+    size_t need_rec = 0;
+    const char* bud_env = getenv("RT_SAMPLE_BUDGET_GB");
+    plan_splat(bud_env ? atof(bud_env)*1e9 : 20.0*(double)s->samp_cap, sp, need_rec);
+    if (!bud_env && (sp.mode != want_mode || need_rec > s->samp_cap)) {
         size_t free_b = 0, total_b = 0;
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
-        budget = (double)free_b + 20.0*(double)s->samp_cap - 16e9;
+        plan_splat((double)free_b + 20.0*(double)s->samp_cap - 16e9, sp, need_rec);
     }
-    SplatCfg sp;
-    sp.passes = spp;
-    sp.mode = g_splat_mode;
-    if (const char* e = getenv("RT_SPLAT")) sp.mode = atoi(e);
-    if (sp.mode == RT_SPLAT_EXACT && (double)total*20.0 > budget) sp.mode = RT_SPLAT_STREAM;
-    if (sp.mode == RT_SPLAT_STREAM && ks > 12) sp.mode = (double)total*20.0 <= budget ? RT_SPLAT_EXACT : RT_SPLAT_ATOMIC;
-    const FrameShape shape = frame_shape(total, spp);
-    size_t need_rec = 0;
-    if (sp.mode == RT_SPLAT_STREAM) {
-        // a resolve every ~32M samples; the ring holds the passes not yet resolved: the chunk,
-        // the claims of the iterations a path can live (about 5 pool fills) and slack
-        const uint32_t per_part = (spp + shape.nparts - 1) / shape.nparts;
-        sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull), per_part);
-        if (const char* e = getenv("RT_SPLAT_CHUNK")) sp.chunk = std::max(1, atoi(e));
-        const unsigned long long lag = (5ull*shape.pool_n + fp.pixels - 1) / fp.pixels;
-        sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, per_part);
-        if (const char* e = getenv("RT_SPLAT_RING")) sp.ring = std::max(1, atoi(e));
-        sp.chunk = std::min(sp.chunk, sp.ring);                      // the planner needs chunk <= ring
-        while (sp.ring > 1 && 20.0*(double)shape.nparts*sp.ring*fp.pixels > budget) {
-            sp.ring = std::max(1u, sp.ring / 2);
-            sp.chunk = std::min(sp.chunk, sp.ring);
-        }
-        need_rec = (size_t)shape.nparts*sp.ring*fp.pixels;
-        if (20.0*(double)need_rec > budget) sp.mode = RT_SPLAT_ATOMIC;
-    }
-    if (sp.mode == RT_SPLAT_EXACT) need_rec = (size_t)total;
     if (sp.mode != RT_SPLAT_ATOMIC && s->samp_cap < need_rec) {
         if (s->d_samp) (void)hipFree(s->d_samp);
         if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
@@ -3548,38 +3593,13 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         }
     }
     if (sp.mode != RT_SPLAT_ATOMIC) {
-        const size_t ntile_all = (size_t)fp.tcx*tcy;
-        std::vector<int32_t> base(ntile_all, -1);
-        for (size_t i = 0; i < ids.size(); ++i) base[ids[i]] = (int32_t)prefix[i];
-        if (s->tile_base_cap < ntile_all) {
-            if (s->d_tile_base) (void)hipFree(s->d_tile_base);
-            s->d_tile_base = nullptr;
-            HIP_OK(hipMalloc(&s->d_tile_base, sizeof(int32_t)*ntile_all));
-            s->tile_base_cap = ntile_all;
-        }
-        HIP_OK(hipMemcpyAsync(s->d_tile_base, base.data(), sizeof(int32_t)*ntile_all, hipMemcpyHostToDevice, stream));
         fp.samp_rgbx = s->d_samp;
         fp.samp_jy = s->d_samp_jy;
         fp.tile_base = s->d_tile_base;
         fp.spp = spp;
         sp.rec = s->d_samp;
         sp.rec_jy = s->d_samp_jy;
-        std::vector<uint32_t> blocks;
-        std::vector<const float4*> part_ptrs;
         if (sp.mode == RT_SPLAT_STREAM) {
-            // output blocks whose source region (the block + the filter radius) meets an owned tile
-            const uint32_t nbx = (w + TR_W - 1) / TR_W, nby = (h + TR_H - 1) / TR_H;
-            for (uint32_t by = 0; by < nby; ++by)
-                for (uint32_t bx = 0; bx < nbx; ++bx) {
-                    const int rx0 = std::max<int>((int)(bx*TR_W) - ks, 0), rx1 = std::min<int>((int)(bx*TR_W + TR_W - 1) + ks, (int)w - 1);
-                    const int ry0 = std::max<int>((int)(by*TR_H) - ks, 0), ry1 = std::min<int>((int)(by*TR_H + TR_H - 1) + ks, (int)h - 1);
-                    bool any = false;
-                    for (int ty = ry0 / (int)fp.tile_h; ty <= ry1 / (int)fp.tile_h && !any; ++ty)
-                        for (int tx = rx0 / (int)fp.tile_w; tx <= rx1 / (int)fp.tile_w && !any; ++tx)
-                            any = base[(size_t)ty*fp.tcx + tx] >= 0;
-                    if (any) blocks.push_back(bx | (by << 16));
-                }
-            sp.nblocks = (uint32_t)blocks.size();
             sp.ksmax = ks <= 2 ? 2 : ks <= 4 ? 4 : 12;
             sp.lds = tr_lds_bytes(sp.ksmax);
             const size_t npx = (size_t)w*h;
@@ -3590,19 +3610,41 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
                 HIP_OK(hipMalloc(&s->d_partials, sizeof(float4)*parts*npx));
                 s->partial_cap = parts*npx;
             }
-            for (size_t k = 0; k < parts; ++k) part_ptrs.push_back(s->d_partials + k*npx);
             sp.partials = s->d_partials;
-            const size_t aux = blocks.size() + 2*MAX_PARTITIONS;           // u32 blocks, then the pointers
-            if (s->aux_cap < aux) {
-                if (s->d_aux) (void)hipFree(s->d_aux);
-                s->d_aux = nullptr; s->aux_cap = 0;
-                HIP_OK(hipMalloc(&s->d_aux, sizeof(uint32_t)*aux));
-                s->aux_cap = aux;
+            if (L.blocks_ks != ks) {
+                // output blocks whose source region (the block + the filter radius) meets an owned tile
+                std::vector<uint32_t> blocks;
+                const uint32_t nbx = (w + TR_W - 1) / TR_W, nby = (h + TR_H - 1) / TR_H;
+                for (uint32_t by = 0; by < nby; ++by)
+                    for (uint32_t bx = 0; bx < nbx; ++bx) {
+                        const int rx0 = std::max<int>((int)(bx*TR_W) - ks, 0), rx1 = std::min<int>((int)(bx*TR_W + TR_W - 1) + ks, (int)w - 1);
+                        const int ry0 = std::max<int>((int)(by*TR_H) - ks, 0), ry1 = std::min<int>((int)(by*TR_H + TR_H - 1) + ks, (int)h - 1);
+                        bool any = false;
+                        for (int ty = ry0 / (int)fp.tile_h; ty <= ry1 / (int)fp.tile_h && !any; ++ty)
+                            for (int tx = rx0 / (int)fp.tile_w; tx <= rx1 / (int)fp.tile_w && !any; ++tx)
+                                any = L.base[(size_t)ty*fp.tcx + tx] >= 0;
+                        if (any) blocks.push_back(bx | (by << 16));
+                    }
+                const size_t aux = blocks.size() + 2*MAX_PARTITIONS;       // the pointer table, then the blocks
+                if (s->aux_cap < aux) {
+                    if (s->d_aux) (void)hipFree(s->d_aux);
+                    s->d_aux = nullptr; s->aux_cap = 0;
+                    HIP_OK(hipMalloc(&s->d_aux, sizeof(uint32_t)*aux));
+                    s->aux_cap = aux;
+                    L.aux_parts = -1;
+                }
+                HIP_OK(hipMemcpy(s->d_aux + 2*MAX_PARTITIONS, blocks.data(), sizeof(uint32_t)*blocks.size(), hipMemcpyHostToDevice));
+                L.nblocks = (uint32_t)blocks.size();
+                L.blocks_ks = ks;
             }
-            uint32_t* d_blocks = s->d_aux + 2*MAX_PARTITIONS;
-            HIP_OK(hipMemcpyAsync(s->d_aux, part_ptrs.data(), sizeof(float4*)*part_ptrs.size(), hipMemcpyHostToDevice, stream));
-            HIP_OK(hipMemcpyAsync(d_blocks, blocks.data(), sizeof(uint32_t)*blocks.size(), hipMemcpyHostToDevice, stream));
-            sp.blocks = d_blocks;
+            if (L.aux_parts != (int)parts || L.aux_partials != s->d_partials || L.aux_npx != npx) {
+                std::vector<const float4*> part_ptrs;
+                for (size_t k = 0; k < parts; ++k) part_ptrs.push_back(s->d_partials + k*npx);
+                if (parts) HIP_OK(hipMemcpy(s->d_aux, part_ptrs.data(), sizeof(float4*)*parts, hipMemcpyHostToDevice));
+                L.aux_parts = (int)parts; L.aux_partials = s->d_partials; L.aux_npx = npx;
+            }
+            sp.nblocks = L.nblocks;
+            sp.blocks = s->d_aux + 2*MAX_PARTITIONS;
             sp.part_ptrs = reinterpret_cast<const float4* const*>(s->d_aux);
             static bool attr_set = false;
             if (!attr_set) {                      // k_resolve_tiles<12> stages up to 72 KB
@@ -3612,10 +3654,10 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
                 attr_set = true;
             }
         }
-        HIP_OK(hipStreamSynchronize(stream));     // `base`, `blocks`, `part_ptrs` are host temporaries
     }
     err = run_frame(s, st, fp, total, stream, sp, stats);
     if (err || sp.mode != RT_SPLAT_EXACT) {
+        if (!err) HIP_OK(hipStreamSynchronize(stream));      // the frame (and its last resolve, combine) is done
         if (stats && !err) stats->splat_mode = sp.mode;
         return err;
     }
