@@ -2760,6 +2760,12 @@ int check_inputs(const rt_settings* st, const rt_filter_cache* f) {
     return RT_OK;
 }
 
+// RT_DEBUG_TIMING=1: host-side timestamps of a frame's setup phases, to stderr.
+inline double host_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+inline bool debug_timing() { static const bool on = getenv("RT_DEBUG_TIMING") != nullptr; return on; }
+
 // Partitions and path pool of a frame of `total` samples (`passes` sample passes over the
 // shard's pixels; 0 = an explicit sample list).  A larger pool amortizes each trace
 // launch's tail (its slowest ray) over more rays, until the pool is so large that the
@@ -2974,11 +2980,15 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         return RT_OK;
     };
     s->cancel = 0;
+    const double t_setup = debug_timing() ? host_ms() : 0.0;
     for (int c = 0; c < 2; ++c)
         for (int k = 0; k < nparts; ++k) {
             int err = enqueue_chunk(k);
             if (err) return err;
         }
+    if (debug_timing())
+        fprintf(stderr, "[rt timing] run_frame: partitions set up %.3f ms, first chunks enqueued %.3f ms\n",
+                t_setup - std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), host_ms() - t_setup);
     uint64_t rounds = 0;
     for (int live = nparts; live > 0; ++rounds) {
         for (int k = 0; k < nparts; ++k) {
@@ -3451,6 +3461,7 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     if (!tiles->tile_w || !tiles->tile_h || !tiles->shard_count || tiles->shard_index >= tiles->shard_count) {
         set_error("bad tile set"); return RT_ERROR_INVALID;
     }
+    const double t_entry = debug_timing() ? host_ms() : 0.0;
     HIP_OK(hipSetDevice(s->device));
     hipStream_t stream = (hipStream_t)hip_stream;
     FrameParams fp = {};
@@ -3655,7 +3666,9 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
             }
         }
     }
+    if (debug_timing()) fprintf(stderr, "[rt timing] rt_render_device: layout + splat plan %.3f ms\n", host_ms() - t_entry);
     err = run_frame(s, st, fp, total, stream, sp, stats);
+    if (debug_timing()) fprintf(stderr, "[rt timing] rt_render_device: frame done %.3f ms after entry\n", host_ms() - t_entry);
     if (err || sp.mode != RT_SPLAT_EXACT) {
         if (!err) HIP_OK(hipStreamSynchronize(stream));      // the frame (and its last resolve, combine) is done
         if (stats && !err) stats->splat_mode = sp.mode;
