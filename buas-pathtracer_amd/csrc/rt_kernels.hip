@@ -117,8 +117,13 @@ extern __shared__ float4 lds_scene[];
 // The scene seen through the LDS copy: every small table's pointer rebased onto
 // `lds` (generic pointers, so the code that reads them is unchanged).  All
 // threads of the block must call it.
+// IN_LDS (the caller launched with the blob in LDS: DevScene::blob_q != 0): the rebased pointers
+// are LDS pointers on every path, so the compiler emits ds_read for the table lookups.  Left to
+// a run-time choice between the copy and HBM, the pointers are generic and every lookup is a
+// FLAT load: a vector-memory instruction that also waits on the LDS counter.
+template <bool IN_LDS = false>
 RT_D DevScene scene_in_lds(const DevScene& sc, float4* lds) {
-    if (!sc.blob_q) return sc;
+    if (!IN_LDS && !sc.blob_q) return sc;
     for (uint32_t i = threadIdx.x; i < sc.blob_q; i += blockDim.x) lds[i] = sc.blob[i];
     __syncthreads();
     DevScene s = sc;
@@ -1709,6 +1714,7 @@ __device__ unsigned long long g_shade_prof[SP_N + 1];
 #define SP_MARK(v)
 #define SP_ADD(i, a)
 #endif
+template <bool IN_LDS>
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur) {
 #if RT_SHADE_PROF
@@ -1729,7 +1735,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         t4 = ldnt(&pool.thr[slot]); L4 = ldnt(&pool.L[slot]); pn4 = ldnt(&pool.prev_n[slot]);
         h4 = ldnt(&pool.hit[slot]); r4 = ldnt(&pool.rng[slot]); hw = ldnt(&pool.hit_w[slot]);
     }
-    const DevScene sc = scene_in_lds(sc_g, lds_scene);
+    const DevScene sc = scene_in_lds<IN_LDS>(sc_g, lds_scene);
     const bool valid = slot < pool.n && state0 == S_TRACE;             // traced this iteration
     bool cont = false, done = false, shadow = false, cast_shadow = false, enq = false;
     Prologue spro = {}, cpro = {};
@@ -2933,7 +2939,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
-        k_shade<<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        if (s->ds.blob_q) k_shade<true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        else k_shade<false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
         if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
