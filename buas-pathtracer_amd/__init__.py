@@ -184,6 +184,13 @@ class Scene:
         if not lib().rth_load_environment_map(self._h, str(path).encode()):
             raise ValueError(lib().rth_last_error().decode())
 
+    def set_environment_map(self, pixels):
+        """An environment map from an (h, w, 3) float32 array (row 0 = v = 0, the bottom)."""
+        a = np.ascontiguousarray(pixels, dtype=np.float32)
+        h, w = a.shape[:2]
+        if not lib().rth_set_environment_map(self._h, w, h, a.ctypes.data_as(C.POINTER(abi.V3))):
+            raise ValueError(lib().rth_last_error().decode())
+
     def create_scene_bvh(self):
         lib().rth_create_scene_bvh(self._h)
 
@@ -319,6 +326,27 @@ class splat_mode:
 
     def __exit__(self, *exc):
         set_splat_mode(abi.RT_SPLAT_STREAM)
+        return False
+
+
+def set_env_sampling(mode):
+    """rt_set_env_sampling: 1 = environment-map importance sampling in the NEE (beyond the
+    reference, whose environment CDF is never read), 0 = the reference's estimator (default)."""
+    _check(lib().rt_set_env_sampling(int(mode)))
+
+
+class env_sampling:
+    """with env_sampling(1): ... turns environment-map sampling off again after."""
+
+    def __init__(self, mode=1):
+        self.mode = mode
+
+    def __enter__(self):
+        set_env_sampling(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        set_env_sampling(0)
         return False
 
 

@@ -179,6 +179,7 @@ ABI_FUNCTIONS = {
     "rt_set_profiling_stages": (C.c_int, [C.c_uint32]),
     "rt_set_path_pool": (C.c_int, [C.c_uint32]),
     "rt_set_splat_mode": (C.c_int, [C.c_int]),
+    "rt_set_env_sampling": (C.c_int, [C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_int, C.c_uint32, P(V3), P(V3), C.c_int, P(BvhNode), P(C.c_uint32), P(C.c_uint32)]),
     "rt_build_bvh_last_error": (C.c_char_p, []),
     "rt_render_picture": (C.c_int, [C.c_void_p, P(Camera), P(Settings), P(FilterCache), P(TileSet), C.c_uint32,
@@ -207,6 +208,7 @@ HOST_FUNCTIONS = {
     "rth_scene_bvh_info": (C.c_int, [C.c_void_p, P(BvhInfo)]),
     "rth_set_sky": (None, [C.c_void_p, V3, V3]),
     "rth_load_environment_map": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "rth_set_environment_map": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(V3)]),
     "rth_create_scene_bvh": (C.c_int, [C.c_void_p]),
     "rth_set_bvh_device": (None, [C.c_int]),
     "rth_build_bvh_entries": (C.c_int, [C.c_uint32, P(V3), P(V3), C.c_int32, P(BvhNode), P(C.c_uint32), P(C.c_uint32)]),

@@ -756,11 +756,26 @@ int rth_load_environment_map(rth_scene* s, const char* path) {              // R
 }
 
 }  // extern "C"
+static void build_sky_cdf(rth_scene* s);
 int rth_load_environment_map_bytes(rth_scene* s, std::vector<char>& file) {
     uint32_t w, h;
     std::vector<rt_v3> px;
     if (!parse_hdr(file, &w, &h, px)) return 0;
     s->sky_w = w; s->sky_h = h; s->sky.swap(px);
+    build_sky_cdf(s);
+    return 1;
+}
+
+extern "C" int rth_set_environment_map(rth_scene* s, uint32_t w, uint32_t h, const rt_v3* pixels) {
+    if (!s || !pixels || !w || !h) { set_err("rth_set_environment_map: empty map"); return 0; }
+    s->sky_w = w; s->sky_h = h;
+    s->sky.assign(pixels, pixels + (size_t)w*h);
+    build_sky_cdf(s);
+    return 1;
+}
+
+static void build_sky_cdf(rth_scene* s) {
+    const uint32_t w = s->sky_w, h = s->sky_h;
     // luma CDF over 32x32 tiles: built exactly like the reference, and (like the
     // reference) never read by the integrator (RT/integrators.cpp:230-233).
     uint32_t tw = w / 32, th = h / 32;
@@ -781,7 +796,6 @@ int rth_load_environment_map_bytes(rth_scene* s, std::vector<char>& file) {
         float rcp = 1.0f / sum;
         for (auto& c : s->sky_cdf) c *= rcp;
     }
-    return 1;
 }
 
 extern "C" {

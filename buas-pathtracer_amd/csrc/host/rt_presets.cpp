@@ -271,7 +271,9 @@ void cornell_box(Ctx& c, uint32_t mesh_tris) {                              // :
     sphere(c, white_light, 1.5f, translate(v3(0, 13.4f, -2)));
 }
 
-void dragon(Ctx& c, uint32_t mesh_tris, bool nested, uint32_t env_seed) {  // :1167-1225
+// unique: the BASELINE C4/C5 "~250k-tri multi-mesh scene" as four distinct meshes (seeds 1..4),
+// so 250k triangles are resident; the reference scene instances one dragon four times.
+void dragon(Ctx& c, uint32_t mesh_tris, bool nested, uint32_t env_seed, bool unique = false) {  // :1167-1225
     camera_basic(c, 40.0f, 6.0f, 1.0f);
     c.cam->p = v3(-25, 6, 0); rth_aim_camera_at(c.cam, v3(1, 5, 0));
     uint32_t ground = add_diffuse(c, v3(0.55f, 0.55f, 0.55f), 1.0f, 0.0f, true);
@@ -291,14 +293,17 @@ void dragon(Ctx& c, uint32_t mesh_tris, bool nested, uint32_t env_seed) {  // :1
     (void)rth_add_emissive_material(c.s, sc(3.0f, v3(1.0f, 10.0f, 2.0f)));
     load_env(c, env_seed);
     uint32_t d = load_mesh(c, mesh_tris, 1);
+    uint32_t d1 = unique ? load_mesh(c, mesh_tris, 2) : d;
+    uint32_t d2 = unique ? load_mesh(c, mesh_tris, 3) : d;
+    uint32_t d3 = unique ? load_mesh(c, mesh_tris, 4) : d;
     rt_m4x4inv t0 = translate(v3(0, 6.0f, 0))*scale(v3(14.0f));
     rt_m4x4inv t1 = translate(v3(-5, 3.7f, 0))*scale(v3(6.0f));
     rt_m4x4inv t2 = translate(v3(-5, 3.7f, -7))*scale(v3(6.0f));
     rt_m4x4inv t3 = translate(v3(-5, 3.7f, 7))*scale(v3(6.0f));
     rth_add_mesh(c.s, blue_glass, d, &t0);
-    rth_add_mesh(c.s, red_glass, d, &t1);
-    rth_add_mesh(c.s, rough, d, &t2);
-    rth_add_mesh(c.s, metal, d, &t3);
+    rth_add_mesh(c.s, red_glass, d1, &t1);
+    rth_add_mesh(c.s, rough, d2, &t2);
+    rth_add_mesh(c.s, metal, d3, &t3);
     box(c, ground, v3(10, 1, 10), translate(v3(0, 1.0f, 0)));
     box(c, ground, v3(40, 1, 40), translate(v3(8.0f, -1.0f, 0)));
     if (nested) {
@@ -411,8 +416,9 @@ extern "C" int rth_load_preset(const char* name_c, uint32_t w, uint32_t h, const
     else if (name == "c1") { week_6(c); st->samples_per_pixel = 16; st->max_bounce_count = 4; }
     else if (name == "c2") { cornell_box(c, 70000); st->samples_per_pixel = 64; }
     else if (name == "c3") { cornell_box(c, 70000); load_env(c, 2); st->samples_per_pixel = 256; }
-    else if (name == "c4") { dragon(c, 62500, true, 3); st->samples_per_pixel = 256; }
-    else if (name == "c5") { dragon(c, 62500, true, 3); st->samples_per_pixel = 1024;
+    else if (name == "c4") { dragon(c, 62500, true, 3, true); st->samples_per_pixel = 256; }
+    else if (name == "c4i") { dragon(c, 62500, true, 3); st->samples_per_pixel = 256; }   // one mesh, 4 instances
+    else if (name == "c5") { dragon(c, 62500, true, 3, true); st->samples_per_pixel = 1024;
                              st->sampling_strategy = RT_SAMPLING_OPTIMIZED_BLUE_NOISE; }
     else ok = false;
     if (!ok) { rth_scene_destroy(s); return 0; }

@@ -40,6 +40,7 @@ void set_error(const std::string& s) { g_error = s; }
 uint32_t g_profiling = 0;       // stage mask: bit k = rt_kernel_stage k timed with HIP events
 uint32_t g_pool_override = 0;
 int g_splat_mode = RT_SPLAT_STREAM;
+int g_env_sampling = 0;         // rt_set_env_sampling
 }
 
 // Tables embedded from data/ (extracted from the reference by tools/extract_tables.py).
@@ -84,6 +85,10 @@ struct DevScene {
     const float4* mnodes4;          // mesh BVH4 nodes (MESH_BVH4), 8 float4 each, global indices
     const float* sky;               // 3 floats per pixel
     uint32_t sky_w, sky_h;
+    // environment-map sampling table (rt_set_env_sampling): per luma tile {alias threshold,
+    // alias tile, density}, env_tx tiles per row of env_tw x env_th texels; null = no map
+    const float4* env_tab;
+    uint32_t env_n, env_tx, env_tw, env_th;
     V3 top_sky, bot_sky;
     const uint8_t* strata;          // g_strata_permutation_sets [256][64]
     const uint8_t* bluenoise;       // sobol | scrambling | ranking
@@ -1017,6 +1022,44 @@ RT_D V3 sample_sky(const DevScene& sc, V3 d) {                           // :272
     }
     return lerp3(sc.bot_sky, sc.top_sky, fabsf(d.y));
 }
+// Environment-map sampling (rt_set_env_sampling; beyond the reference, whose CDF of
+// RT/assets.cpp:620-665 is never read, RT/integrators.cpp:230-233).  The table has one
+// entry per luma tile of load_environment_map's grid: {alias threshold, alias tile,
+// density}, density = the tile's luma share x texels / tile texels (a pdf over the
+// unit (u, v) square).  A sample is one 16-byte read: tile k = floor(e n) or its alias.
+RT_D V3 env_direction(const DevScene& sc, float e, V2 s2) {
+    const float fe = e*(float)sc.env_n;
+    uint32_t k = (uint32_t)fe;
+    if (k >= sc.env_n) k = sc.env_n - 1;
+    const float frac = fe - (float)k;
+    const float4 ent = sc.env_tab[k];
+    const uint32_t tile = frac < ent.x ? k : __float_as_uint(ent.y);
+    const uint32_t x0 = (tile % sc.env_tx)*sc.env_tw, y0 = (tile / sc.env_tx)*sc.env_th;
+    const uint32_t cw = min(sc.env_tw, sc.sky_w - x0), ch = min(sc.env_th, sc.sky_h - y0);
+    const float u = ((float)x0 + s2.x*(float)cw) / (float)sc.sky_w;
+    const float v = ((float)y0 + s2.y*(float)ch) / (float)sc.sky_h;
+    const float phi = (u - 0.5f)*(2.0f*PI_32), theta = (v - 0.5f)*PI_32;   // sample_sky's mapping inverted
+    const float ct = d_cosf(theta);
+    return {ct*d_cosf(phi), d_sinf(theta), ct*d_sinf(phi)};
+}
+// sample_sky's texel for d, and the table tile it lies in
+RT_D V3 sky_env(const DevScene& sc, V3 d, uint32_t& tile) {
+    const float rcp_pi = 1.0f / PI_32;
+    const float rcp_2pi = 0.5f / PI_32;
+    const float u = 0.5f + rcp_2pi*d_atan2f(d.z, d.x);
+    const float v = 0.5f + rcp_pi*d_asinf(d.y);
+    const uint32_t sx = (uint32_t)(int32_t)(u*(float)sc.sky_w) % sc.sky_w;
+    const uint32_t sy = (uint32_t)(int32_t)(v*(float)sc.sky_h) % sc.sky_h;
+    tile = (sy / sc.env_th)*sc.env_tx + sx / sc.env_tw;
+    const float* p = sc.sky + 3*((size_t)sy*sc.sky_w + sx);
+    return {p[0], p[1], p[2]};
+}
+// solid-angle pdf of env_direction at d (in `tile`): density / (2 pi^2 cos theta)
+RT_D float env_pdf(const DevScene& sc, uint32_t tile, V3 d) {
+    const float c2 = 1.0f - d.y*d.y;
+    if (!(c2 > 0.0f)) return 0.0f;
+    return sc.env_tab[tile].z / ((2.0f*PI_32*PI_32)*__builtin_sqrtf(c2));
+}
 RT_D V3 evaluate_material(const rt_material& m, V3 p) {                 // :297-308
     if (m.flags & RT_MATERIAL_CHECKERS) {
         int32_t ch = (((int32_t)floorf(0.25f*p.x)) ^ ((int32_t)floorf(0.25f*p.z))) & 1;
@@ -1714,7 +1757,8 @@ __device__ unsigned long long g_shade_prof[SP_N + 1];
 #define SP_MARK(v)
 #define SP_ADD(i, a)
 #endif
-template <bool IN_LDS>
+// ENV: rt_set_env_sampling on, the scene has an environment map and NEE is on
+template <bool IN_LDS, bool ENV>
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur) {
 #if RT_SHADE_PROF
@@ -1837,44 +1881,69 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                     is_spec = 0;
                     V3 albedo = evaluate_material(mt, I);
                     V3 brdf = smul(1.0f / PI_32, albedo);
-                    if (st.next_event_estimation && sc.light_count > 0) {      // NEE :738-771
+                    if (st.next_event_estimation && (sc.light_count > 0 || ENV)) {      // NEE :738-771
                         float lps = sample_1d(sc, ss, rng, S_LightSelection, bounce);
+                        // ENV: the environment is picked with probability q (1 without lights)
+                        const float q = sc.light_count > 0 ? 0.5f : 1.0f;
+                        const bool pick_env = ENV && lps < q;
+                        if (ENV) lps = pick_env ? lps / q : (lps - q) / (1.0f - q);
                         float lrp = 0.0f;
-                        uint32_t lid = pick_random_light(sc, st, lps, I, lrp);
-                        const rt_primitive light = sc.prims[lid];
+                        uint32_t lid = pick_env ? 0u : pick_random_light(sc, st, lps, I, lrp);
+                        if (ENV) lrp = lrp*(1.0f - q);
                         V2 s2 = sample_2d(sc, ss, rng, S_DirectLighting, bounce);
-                        // random_point_on_light (:199-228), sphere lights
-                        const M34 lf = load_m34(&sc.fwd[light.transform_index]);
-                        V3 towards = normalize(sub(translation(lf), I));
-                        if (light.type == RT_PRIMITIVE_SPHERE) {
-                            float rad = light.p[0];
-                            V3 Nl = map_to_hemisphere(neg(towards), s2);
-                            V3 pw = xform(lf, muls(Nl, rad), 1.0f);
-                            V3 Lv = sub(pw, I);
-                            float dsq = length_sq(Lv);
-                            float dist = __builtin_sqrtf(dsq);
-                            Lv = divs(Lv, dist);
-                            float A = 2.0f*PI_32*rad*rad;
+                        if (pick_env) {
+                            V3 Lv = env_direction(sc, lps, s2);
                             float ndl = dot(N, Lv);
-                            float nndl = -dot(Nl, Lv);
-                            if (ndl > 0.0f && nndl > 0.0f) {
-                                float sa = (nndl * A) / dsq;
-                                float pdf;
-                                if (st.use_mis) {
-                                    float lpdf = rcp_cr(sa);
+                            if (ndl > 0.0f) {
+                                uint32_t tile;
+                                V3 Le = sky_env(sc, Lv, tile);
+                                float pe = env_pdf(sc, tile, Lv);
+                                if (pe > 0.0f) {
                                     float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
-                                    pdf = lpdf + bpdf;
-                                } else {
-                                    pdf = rcp_cr(sa);
+                                    float pdf = st.use_mis ? q*pe + bpdf : q*pe;
+                                    sh_c = mul(mul(muls(thr, ndl / pdf), brdf), Le);
+                                    sh_o = add(I, muls(Lv, EPSILON));
+                                    sh_d = Lv;
+                                    sh_t = FLT_MAX_;
+                                    sh_light = 0;                   // the null primitive: nothing ignored
+                                    cast_shadow = true;
                                 }
-                                pdf *= lrp;
-                                sh_c = mul(mul(muls(thr, dot(N, Lv) / pdf), brdf),
-                                           rv3(sc.materials[light.material_id].emission_color));
-                                sh_o = add(I, muls(Lv, EPSILON));
-                                sh_d = Lv;
-                                sh_t = dist - 2*EPSILON;
-                                sh_light = lid;
-                                cast_shadow = true;                 // traced below, lanes reconverged
+                            }
+                        } else {
+                            // random_point_on_light (:199-228), sphere lights
+                            const rt_primitive light = sc.prims[lid];
+                            const M34 lf = load_m34(&sc.fwd[light.transform_index]);
+                            V3 towards = normalize(sub(translation(lf), I));
+                            if (light.type == RT_PRIMITIVE_SPHERE) {
+                                float rad = light.p[0];
+                                V3 Nl = map_to_hemisphere(neg(towards), s2);
+                                V3 pw = xform(lf, muls(Nl, rad), 1.0f);
+                                V3 Lv = sub(pw, I);
+                                float dsq = length_sq(Lv);
+                                float dist = __builtin_sqrtf(dsq);
+                                Lv = divs(Lv, dist);
+                                float A = 2.0f*PI_32*rad*rad;
+                                float ndl = dot(N, Lv);
+                                float nndl = -dot(Nl, Lv);
+                                if (ndl > 0.0f && nndl > 0.0f) {
+                                    float sa = (nndl * A) / dsq;
+                                    float pdf;
+                                    if (st.use_mis) {
+                                        float lpdf = rcp_cr(sa);
+                                        float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
+                                        pdf = lpdf + bpdf;
+                                    } else {
+                                        pdf = rcp_cr(sa);
+                                    }
+                                    pdf *= lrp;
+                                    sh_c = mul(mul(muls(thr, dot(N, Lv) / pdf), brdf),
+                                               rv3(sc.materials[light.material_id].emission_color));
+                                    sh_o = add(I, muls(Lv, EPSILON));
+                                    sh_d = Lv;
+                                    sh_t = dist - 2*EPSILON;
+                                    sh_light = lid;
+                                    cast_shadow = true;                 // traced below, lanes reconverged
+                                }
                             }
                         }
                     }
@@ -1909,7 +1978,26 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             }
         } else {
             SP_MARK(t_sky);
-            total = add(total, mul(thr, sample_sky(sc, rd)));                 // miss :812-815
+            if (ENV) {
+                // a path leaving a diffuse vertex (which sampled the environment in its NEE):
+                // balance heuristic against that pdf; without MIS the NEE alone carries it
+                uint32_t tile;
+                V3 Le = sky_env(sc, rd, tile);
+                if (!is_spec) {
+                    float wgt = 0.0f;
+                    if (st.use_mis) {
+                        const float q = sc.light_count > 0 ? 0.5f : 1.0f;
+                        float pe = env_pdf(sc, tile, rd);
+                        float bpdf = (st.importance_sample_diffuse ? dot(prev_N, rd) / PI_32 : 1.0f / (2.0f*PI_32));
+                        float den = q*pe + bpdf;
+                        wgt = den > 0.0f ? bpdf / den : 0.0f;
+                    }
+                    Le = smul(wgt, Le);
+                }
+                total = add(total, mul(thr, Le));
+            } else {
+                total = add(total, mul(thr, sample_sky(sc, rd)));             // miss :812-815
+            }
             done = true;
             SP_ADD(SP_SKY, t_sky);
         }
@@ -2926,6 +3014,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             }
         }
     };
+    // environment-map NEE (rt_set_env_sampling): only with a map, its table and NEE
+    const bool env = g_env_sampling && s->ds.env_tab && st->next_event_estimation;
     auto iterate = [&](int k, bool plan) {
         Partition& pt = s->part[k];
         Run& r = run[k];
@@ -2939,8 +3029,14 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
-        if (s->ds.blob_q) k_shade<true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
-        else k_shade<false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        if (env) {
+            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        } else if (s->ds.blob_q) {
+            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        } else {
+            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
         if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
@@ -3109,6 +3205,63 @@ int bind_device(int device) {
     return RT_OK;
 }
 
+// The environment-map sampling table (rt_set_env_sampling, env_direction).  Tiles are
+// load_environment_map's grid (RT/assets.cpp:620-665): tile_w = w / 32, tile_h = h / 32,
+// row-major, a tile's luma (0.299 r + 0.587 g + 0.114 b, RT/common.h:142-145) summed in texel
+// order.  A tile is drawn with probability luma / total through an alias table (Vose's
+// method); its density over the unit (u, v) square is that probability x texels / tile texels.
+// No table (false) for maps under 32 x 32 texels, negative luma or no light at all.
+bool build_env_table(uint32_t w, uint32_t h, const rt_v3* px, std::vector<float4>& tab,
+                     uint32_t& tx, uint32_t& tw, uint32_t& th) {
+    if (!px || w < 32 || h < 32) return false;
+    tw = w / 32; th = h / 32;
+    tx = (w + tw - 1) / tw;
+    const uint32_t ty = (h + th - 1) / th, n = tx*ty;
+    std::vector<float> lum(n), scaled(n), prob(n, 1.0f);
+    std::vector<uint32_t> alias(n);
+    float sum = 0.0f;
+    for (uint32_t t = 0; t < n; ++t) {
+        const uint32_t x0 = (t % tx)*tw, y0 = (t / tx)*th;
+        const uint32_t x1 = std::min(x0 + tw, w), y1 = std::min(y0 + th, h);
+        float cur = 0.0f;
+        for (uint32_t y = y0; y < y1; ++y)
+            for (uint32_t x = x0; x < x1; ++x) {
+                const rt_v3& c = px[(size_t)y*w + x];
+                cur += 0.299f*c.x + 0.587f*c.y + 0.114f*c.z;
+            }
+        if (!(cur >= 0.0f)) return false;
+        lum[t] = cur;
+        sum += cur;
+    }
+    if (!(sum > 0.0f) || !std::isfinite(sum)) return false;
+    const float rcp = 1.0f / sum;
+    tab.assign(n, make_float4(0, 0, 0, 0));
+    std::vector<uint32_t> small, large;
+    for (uint32_t t = 0; t < n; ++t) {
+        const uint32_t x0 = (t % tx)*tw, y0 = (t / tx)*th;
+        const uint32_t cw = std::min(x0 + tw, w) - x0, ch = std::min(y0 + th, h) - y0;
+        const float p = lum[t]*rcp;
+        tab[t].z = p*((float)((uint64_t)w*h) / (float)(cw*ch));
+        scaled[t] = p*(float)n;
+        alias[t] = t;
+        (scaled[t] < 1.0f ? small : large).push_back(t);
+    }
+    while (!small.empty() && !large.empty()) {
+        const uint32_t l = small.back(), g = large.back();
+        small.pop_back(); large.pop_back();
+        prob[l] = scaled[l];
+        alias[l] = g;
+        scaled[g] = (scaled[g] + scaled[l]) - 1.0f;
+        (scaled[g] < 1.0f ? small : large).push_back(g);
+    }
+    for (uint32_t t = 0; t < n; ++t) {
+        tab[t].x = prob[t];
+        uint32_t a = alias[t];
+        memcpy(&tab[t].y, &a, 4);
+    }
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -3126,6 +3279,12 @@ int rt_device_count(int* out) {
 int rt_set_profiling(int enable) { g_profiling = enable ? (1u << RT_KERNEL_COUNT) - 1u : 0u; return RT_OK; }
 int rt_set_profiling_stages(uint32_t mask) { g_profiling = mask & ((1u << RT_KERNEL_COUNT) - 1u); return RT_OK; }
 int rt_set_path_pool(uint32_t paths) { g_pool_override = paths; return RT_OK; }
+int rt_set_env_sampling(int mode) {
+    if (mode != 0 && mode != 1) { set_error("rt_set_env_sampling: mode must be 0 or 1"); return RT_ERROR_INVALID; }
+    g_env_sampling = mode;
+    return RT_OK;
+}
+
 int rt_set_splat_mode(int mode) {
     if (mode < RT_SPLAT_STREAM || mode > RT_SPLAT_ATOMIC) { set_error("bad splat mode"); return RT_ERROR_INVALID; }
     g_splat_mode = mode;
@@ -3337,6 +3496,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     if (d->skydome && d->skydome_w && d->skydome_h) {
         if ((err = upload(s, reinterpret_cast<const float*>(d->skydome), 3*(size_t)d->skydome_w*d->skydome_h, &ds.sky))) return fail(err);
         ds.sky_w = d->skydome_w; ds.sky_h = d->skydome_h;
+        std::vector<float4> et;
+        if (build_env_table(d->skydome_w, d->skydome_h, d->skydome, et, ds.env_tx, ds.env_tw, ds.env_th)) {
+            if ((err = upload(s, et.data(), et.size(), &ds.env_tab))) return fail(err);
+            ds.env_n = (uint32_t)et.size();
+        }
     }
     ds.top_sky = rv3(d->top_sky_color);
     ds.bot_sky = rv3(d->bot_sky_color);

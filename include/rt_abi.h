@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status */
 enum rt_status {
@@ -372,6 +372,22 @@ enum rt_splat_mode {
     RT_SPLAT_ATOMIC = 2,
 };
 int rt_set_splat_mode(int mode);
+
+/* Environment-map importance sampling for next event estimation; 0 (default) = off.
+ * The reference builds a luma CDF over 32 x 32 tiles of the environment map
+ * (load_environment_map, RT/assets.cpp:620-665) but never samples it
+ * (sample_environment_map is a stub, RT/integrators.cpp:230-233), so mode 0 is the
+ * reference's estimator.  Mode 1, for scenes with an environment map and with
+ * next_event_estimation on: a diffuse vertex's NEE picks the environment with probability
+ * 1/2 (1 when the scene has no lights; a sphere light is then picked as before, its
+ * probability halved), draws a tile with probability proportional to its luma (an alias
+ * table built from the same tile sums at rt_scene_upload) and a uniform point in it, and
+ * casts an unbounded shadow ray.  A path that leaves a diffuse vertex and escapes is
+ * weighted against that pdf by the balance heuristic (use_mis; without MIS the
+ * environment reaches diffuse vertices through the NEE only, as lights do in the
+ * reference).  The estimate's expectation is unchanged; its noise is not the reference's.
+ * No effect for scenes without an environment map (or one under 32 x 32 texels). */
+int rt_set_env_sampling(int mode);
 
 /* discard_current_render (RT/raytracer.cpp:686-690): polled between wavefront
  * iterations; the render in flight returns RT_ERROR_CANCELLED. */

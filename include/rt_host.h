@@ -86,6 +86,8 @@ int      rth_scene_bvh_info(rth_scene* s, rth_bvh_info* out);
 void     rth_set_sky(rth_scene* s, rt_v3 top, rt_v3 bot);
 /* load_environment_map: parse_hdr + luma CDF (the CDF is built, as in the reference) */
 int      rth_load_environment_map(rth_scene* s, const char* hdr_path);
+/* The same from pixels in memory (w*h, row 0 = the bottom row sample_sky reads at v = 0) */
+int      rth_set_environment_map(rth_scene* s, uint32_t w, uint32_t h, const rt_v3* pixels);
 
 /* Build the BVHs of rth_create_mesh / rth_create_scene_bvh on `device` with rt_build_bvh
  * (midpoint and binned SAH; bit-identical to the host builder); -1 (the default): on the host.

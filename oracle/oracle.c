@@ -658,12 +658,91 @@ static int intersect_scene_internal(const rt_scene_desc* scene, const Ray* ray, 
 /* Integrator (RT/integrators.cpp)                                        */
 /* ====================================================================== */
 
+/* Environment-map sampling table (oracle_set_env_sampling; rt_set_env_sampling in
+   include/rt_abi.h).  Beyond the reference: load_environment_map builds a tile luma CDF
+   (RT/assets.cpp:620-665) that nothing reads (RT/integrators.cpp:230-233).  The tiles are
+   that CDF's grid; the table is the alias form of the same tile sums. */
+typedef struct {
+    uint32_t n, tx, tw, th;
+    float* prob;          /* alias threshold */
+    uint32_t* alias;
+    float* dens;          /* tile probability x texels / tile texels: pdf over the (u, v) square */
+} EnvTab;
+
 typedef struct {
     const rt_scene_desc* scene;
     const rt_settings* settings;
     const rt_material* air;
     uint64_t closest_rays, shadow_rays;
+    const EnvTab* env;    /* NULL: the reference's estimator */
 } Ctx;
+
+static int g_env_sampling = 0;
+void oracle_set_env_sampling(int mode) { g_env_sampling = mode != 0; }
+
+static void env_tab_free(EnvTab* t) {
+    free(t->prob); free(t->alias); free(t->dens);
+    memset(t, 0, sizeof(*t));
+}
+
+/* tile luma sums in load_environment_map's order (RT/assets.cpp:634-656, luma RT/common.h:142),
+   probabilities luma / total, Vose's alias construction (stacks popped from the end) */
+static int env_tab_build(const rt_scene_desc* sc, EnvTab* t) {
+    memset(t, 0, sizeof(*t));
+    const uint32_t w = sc->skydome_w, h = sc->skydome_h;
+    if (!sc->skydome || w < 32 || h < 32) return 0;
+    t->tw = w / 32; t->th = h / 32;
+    t->tx = (w + t->tw - 1) / t->tw;
+    const uint32_t ty = (h + t->th - 1) / t->th, n = t->tx*ty;
+    t->n = n;
+    float* lum = (float*)malloc(sizeof(float)*n);
+    float* scaled = (float*)malloc(sizeof(float)*n);
+    uint32_t* small = (uint32_t*)malloc(sizeof(uint32_t)*n);
+    uint32_t* large = (uint32_t*)malloc(sizeof(uint32_t)*n);
+    t->prob = (float*)malloc(sizeof(float)*n);
+    t->alias = (uint32_t*)malloc(sizeof(uint32_t)*n);
+    t->dens = (float*)malloc(sizeof(float)*n);
+    float sum = 0.0f;
+    int ok = 1;
+    for (uint32_t k = 0; k < n && ok; ++k) {
+        uint32_t x0 = (k % t->tx)*t->tw, y0 = (k / t->tx)*t->th;
+        uint32_t x1 = x0 + t->tw < w ? x0 + t->tw : w, y1 = y0 + t->th < h ? y0 + t->th : h;
+        float cur = 0.0f;
+        for (uint32_t y = y0; y < y1; ++y)
+            for (uint32_t x = x0; x < x1; ++x) {
+                const rt_v3* c = &sc->skydome[(size_t)y*w + x];
+                cur += 0.299f*c->x + 0.587f*c->y + 0.114f*c->z;
+            }
+        if (!(cur >= 0.0f)) ok = 0;
+        lum[k] = cur;
+        sum += cur;
+    }
+    if (!ok || !(sum > 0.0f) || !isfinite(sum)) ok = 0;
+    if (ok) {
+        float rcp = 1.0f / sum;
+        uint32_t ns = 0, nl = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            uint32_t x0 = (k % t->tx)*t->tw, y0 = (k / t->tx)*t->th;
+            uint32_t cw = (x0 + t->tw < w ? x0 + t->tw : w) - x0, ch = (y0 + t->th < h ? y0 + t->th : h) - y0;
+            float p = lum[k]*rcp;
+            t->dens[k] = p*((float)((uint64_t)w*h) / (float)(cw*ch));
+            scaled[k] = p*(float)n;
+            t->prob[k] = 1.0f;
+            t->alias[k] = k;
+            if (scaled[k] < 1.0f) small[ns++] = k; else large[nl++] = k;
+        }
+        while (ns && nl) {
+            uint32_t l = small[--ns], g = large[--nl];
+            t->prob[l] = scaled[l];
+            t->alias[l] = g;
+            scaled[g] = (scaled[g] + scaled[l]) - 1.0f;
+            if (scaled[g] < 1.0f) small[ns++] = g; else large[nl++] = g;
+        }
+    }
+    free(lum); free(scaled); free(small); free(large);
+    if (!ok) env_tab_free(t);
+    return ok;
+}
 
 static V3 random_in_unit_sphere(RandomSeries* e) {            /* :11-19 */
     V3 r; float u[4];
@@ -804,6 +883,43 @@ static V3 sample_sky(const rt_scene_desc* sc, const Ray* ray) {              /* 
     return lerp3(sc->bot_sky_color, sc->top_sky_color, st);
 }
 
+/* a direction from the table: tile k = floor(e n) or its alias, a uniform point of the tile
+   (s2), sample_sky's (u, v) mapping inverted */
+static V3 env_direction(const EnvTab* t, const rt_scene_desc* sc, float e, V2 s2) {
+    float fe = e*(float)t->n;
+    uint32_t k = (uint32_t)fe;
+    if (k >= t->n) k = t->n - 1;
+    float frac = fe - (float)k;
+    uint32_t tile = frac < t->prob[k] ? k : t->alias[k];
+    uint32_t x0 = (tile % t->tx)*t->tw, y0 = (tile / t->tx)*t->th;
+    uint32_t cw = t->tw < sc->skydome_w - x0 ? t->tw : sc->skydome_w - x0;
+    uint32_t ch = t->th < sc->skydome_h - y0 ? t->th : sc->skydome_h - y0;
+    float u = ((float)x0 + s2.x*(float)cw) / (float)sc->skydome_w;
+    float v = ((float)y0 + s2.y*(float)ch) / (float)sc->skydome_h;
+    float phi = (u - 0.5f)*(2.0f*PI_32), theta = (v - 0.5f)*PI_32;
+    float ct = cosf_(theta);
+    return v3(ct*cosf_(phi), sinf_(theta), ct*sinf_(phi));
+}
+
+/* sample_sky's texel for d and its tile */
+static V3 sky_env(const EnvTab* t, const rt_scene_desc* sc, V3 d, uint32_t* tile) {
+    float rcp_pi = 1.0f / PI_32;
+    float rcp_2pi = 0.5f / PI_32;
+    float u = 0.5f + rcp_2pi*atan2f_(d.z, d.x);
+    float v = 0.5f + rcp_pi*asinf_(d.y);
+    uint32_t sx = (uint32_t)(int32_t)(u*(float)sc->skydome_w) % sc->skydome_w;
+    uint32_t sy = (uint32_t)(int32_t)(v*(float)sc->skydome_h) % sc->skydome_h;
+    *tile = (sy / t->th)*t->tx + sx / t->tw;
+    return sc->skydome[(size_t)sy*sc->skydome_w + sx];
+}
+
+/* solid-angle pdf of env_direction: density / (2 pi^2 cos theta) */
+static float env_pdf(const EnvTab* t, uint32_t tile, V3 d) {
+    float c2 = 1.0f - d.y*d.y;
+    if (!(c2 > 0.0f)) return 0.0f;
+    return t->dens[tile] / ((2.0f*PI_32*PI_32)*sqrtf(c2));
+}
+
 static inline V3 evaluate_material(const rt_material* m, V3 p) {            /* :297-308 */
     V3 r = m->albedo;
     if (m->flags & RT_MATERIAL_CHECKERS) {
@@ -905,35 +1021,62 @@ static V3 advanced_integrator(Ctx* ctx, Sampler* sampler, RandomSeries* entropy,
                         is_specular = 0;
                         V3 albedo = evaluate_material(mt, I);
                         V3 brdf = smul(1.0f / PI_32, albedo);
-                        if (st->next_event_estimation && scene->light_count > 0) {
+                        const int env = ctx->env != NULL;
+                        if (st->next_event_estimation && (scene->light_count > 0 || env)) {
                             float lps = get_next_sample_1d(sampler, Sample_LightSelection, bounce);
+                            /* env: the environment is picked with probability q (1 without lights) */
+                            const float q = scene->light_count > 0 ? 0.5f : 1.0f;
+                            const int pick_env = env && lps < q;
+                            if (env) lps = pick_env ? lps / q : (lps - q) / (1.0f - q);
                             float lrp = 0.0f;
-                            uint32_t lid = pick_random_light(ctx, lps, I, &lrp);
-                            const rt_primitive* light = &scene->primitives[lid];
-                            const rt_material* lmat = &scene->materials[light->material_id];
+                            uint32_t lid = pick_env ? 0u : pick_random_light(ctx, lps, I, &lrp);
+                            if (env) lrp = lrp*(1.0f - q);
                             V2 s2 = get_next_sample_2d(sampler, Sample_DirectLighting, bounce);
-                            LightSample ls = random_point_on_light(ctx, light, s2, I);
-                            V3 L = ls.L, Nl = ls.Nl;
-                            float ndl = dot(N, L);
-                            float nndl = -dot(Nl, L);
-                            if (ndl > 0.0f && nndl > 0.0f) {
-                                Hit sh;
-                                Ray sray = make_ray(add(I, muls(L, EPSILON)), L, ls.dist - 2*EPSILON);
-                                ctx->shadow_rays++;
-                                if (!intersect_scene_internal(scene, &sray, 1, lid, &sh)) {
-                                    float sa = (nndl * ls.A) / ls.dist_sq;
-                                    float pdf;
-                                    if (st->use_mis) {
-                                        float lpdf = 1.0f / sa;
-                                        float bpdf = (st->importance_sample_diffuse ? ndl / PI_32
-                                                                                    : 1.0f / (2.0f*PI_32));
-                                        pdf = lpdf + bpdf;
-                                    } else {
-                                        pdf = 1.0f / sa;
+                            if (pick_env) {
+                                V3 L = env_direction(ctx->env, scene, lps, s2);
+                                float ndl = dot(N, L);
+                                if (ndl > 0.0f) {
+                                    uint32_t tile;
+                                    V3 Le = sky_env(ctx->env, scene, L, &tile);
+                                    float pe = env_pdf(ctx->env, tile, L);
+                                    if (pe > 0.0f) {
+                                        Hit sh;
+                                        Ray sray = make_ray(add(I, muls(L, EPSILON)), L, FLT_MAX);
+                                        ctx->shadow_rays++;
+                                        if (!intersect_scene_internal(scene, &sray, 1, 0, &sh)) {
+                                            float bpdf = (st->importance_sample_diffuse ? ndl / PI_32
+                                                                                        : 1.0f / (2.0f*PI_32));
+                                            float pdf = st->use_mis ? q*pe + bpdf : q*pe;
+                                            total = add(total, mul(mul(muls(thr, ndl / pdf), brdf), Le));
+                                        }
                                     }
-                                    pdf *= lrp;
-                                    V3 contrib = mul(mul(muls(thr, dot(N, ls.L) / pdf), brdf), lmat->emission_color);
-                                    total = add(total, contrib);
+                                }
+                            } else {
+                                const rt_primitive* light = &scene->primitives[lid];
+                                const rt_material* lmat = &scene->materials[light->material_id];
+                                LightSample ls = random_point_on_light(ctx, light, s2, I);
+                                V3 L = ls.L, Nl = ls.Nl;
+                                float ndl = dot(N, L);
+                                float nndl = -dot(Nl, L);
+                                if (ndl > 0.0f && nndl > 0.0f) {
+                                    Hit sh;
+                                    Ray sray = make_ray(add(I, muls(L, EPSILON)), L, ls.dist - 2*EPSILON);
+                                    ctx->shadow_rays++;
+                                    if (!intersect_scene_internal(scene, &sray, 1, lid, &sh)) {
+                                        float sa = (nndl * ls.A) / ls.dist_sq;
+                                        float pdf;
+                                        if (st->use_mis) {
+                                            float lpdf = 1.0f / sa;
+                                            float bpdf = (st->importance_sample_diffuse ? ndl / PI_32
+                                                                                        : 1.0f / (2.0f*PI_32));
+                                            pdf = lpdf + bpdf;
+                                        } else {
+                                            pdf = 1.0f / sa;
+                                        }
+                                        pdf *= lrp;
+                                        V3 contrib = mul(mul(muls(thr, dot(N, ls.L) / pdf), brdf), lmat->emission_color);
+                                        total = add(total, contrib);
+                                    }
                                 }
                             }
                         }
@@ -960,7 +1103,27 @@ static V3 advanced_integrator(Ctx* ctx, Sampler* sampler, RandomSeries* entropy,
                 }
             }
         } else {
-            total = add(total, mul(thr, sample_sky(scene, &ray)));
+            if (ctx->env) {
+                /* leaving a diffuse vertex, which sampled the environment in its NEE: balance
+                   heuristic against that pdf; without MIS the NEE alone carries it */
+                uint32_t tile;
+                V3 Le = sky_env(ctx->env, scene, ray.d, &tile);
+                if (!is_specular) {
+                    float wgt = 0.0f;
+                    if (st->use_mis) {
+                        const float q = scene->light_count > 0 ? 0.5f : 1.0f;
+                        float pe = env_pdf(ctx->env, tile, ray.d);
+                        float bpdf = (st->importance_sample_diffuse ? dot(prev_N, ray.d) / PI_32
+                                                                    : 1.0f / (2.0f*PI_32));
+                        float den = q*pe + bpdf;
+                        wgt = den > 0.0f ? bpdf / den : 0.0f;
+                    }
+                    Le = smul(wgt, Le);
+                }
+                total = add(total, mul(thr, Le));
+            } else {
+                total = add(total, mul(thr, sample_sky(scene, &ray)));
+            }
             break;
         }
         prev_N = N;
@@ -1118,6 +1281,7 @@ typedef struct {
     atomic_uint next;
     atomic_ullong closest, shadow;
     rt_material air;
+    const EnvTab* env;
 } Job;
 
 static void tile_window(const Job* J, uint32_t tile, int64_t* wx0, int64_t* wy0, int64_t* ww, int64_t* wh) {
@@ -1135,7 +1299,7 @@ static void tile_window(const Job* J, uint32_t tile, int64_t* wx0, int64_t* wy0,
 }
 
 static void render_tile(Job* J, uint32_t tile, float* win, int64_t wx0, int64_t wy0, int64_t ww) {
-    Ctx ctx = { J->scene, J->settings, &J->air, 0, 0 };
+    Ctx ctx = { J->scene, J->settings, &J->air, 0, 0, J->env };
     const rt_settings* st = J->settings;
     uint32_t min_x = J->tile_w*(tile % J->tcx), min_y = J->tile_h*(tile / J->tcx);
     uint32_t max_x = min_x + J->tile_w < J->w ? min_x + J->tile_w : J->w;
@@ -1228,6 +1392,9 @@ int oracle_render_tiles(const rt_scene_desc* scene, const rt_camera* camera, con
     J->rng_mode = rng_mode;
     J->tiles = tile_list; J->tile_count = tile_list_count;
     init_air(&J->air);
+    EnvTab env;
+    const int have_env = g_env_sampling && settings->next_event_estimation && env_tab_build(scene, &env);
+    J->env = have_env ? &env : NULL;
     atomic_init(&J->next, 0u);
     atomic_init(&J->closest, 0ull);
     atomic_init(&J->shadow, 0ull);
@@ -1270,6 +1437,7 @@ int oracle_render_tiles(const rt_scene_desc* scene, const rt_camera* camera, con
         stats->iterations = 0;
         stats->seconds = now_s() - t0;
     }
+    if (have_env) env_tab_free(&env);
     free(J);
     return RT_OK;
 }
@@ -1306,7 +1474,9 @@ int oracle_trace_samples(const rt_scene_desc* scene, const rt_camera* camera, co
     if (err) return err;
     rt_material air;
     init_air(&air);
-    Ctx ctx = { scene, settings, &air, 0, 0 };
+    EnvTab env;
+    const int have_env = g_env_sampling && settings->next_event_estimation && env_tab_build(scene, &env);
+    Ctx ctx = { scene, settings, &air, 0, 0, have_env ? &env : NULL };
     CamSetup c = cam_setup(camera, w, h);
     uint32_t tcx = (w + tile_w - 1) / tile_w;
     for (uint32_t i = 0; i < count; ++i) {
@@ -1322,6 +1492,7 @@ int oracle_trace_samples(const rt_scene_desc* scene, const rt_camera* camera, co
         out[5*i + 0] = r.x; out[5*i + 1] = r.y; out[5*i + 2] = r.z;
         out[5*i + 3] = jx; out[5*i + 4] = jy;
     }
+    if (have_env) env_tab_free(&env);
     if (stats) {
         stats->closest_hit_rays = ctx.closest_rays;
         stats->shadow_rays = ctx.shadow_rays;

@@ -86,6 +86,8 @@ float    oracle_atan2f(float y, float x);
 float    oracle_asinf(float x);
 /* 0 = deterministic spec transcendentals (default), 1 = C library (pins vs the reference) */
 void     oracle_set_math_mode(int libm);
+/* 1 = environment-map sampling in the NEE, as rt_set_env_sampling (include/rt_abi.h); 0 = off */
+void     oracle_set_env_sampling(int mode);
 /* Mitchell–Netravali and friends (RT/reconstruction_filters.cpp:8-95) + LUT */
 int      oracle_load_filter(const char* name, rt_filter_cache* out);
 

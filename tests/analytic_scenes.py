@@ -139,3 +139,42 @@ def disc_fraction(w, h, r=3.0, dist=10.0, vfov_deg=30.0):
     ang = math.asin(r / dist)                     # angular radius of the sphere
     rad_film = film_d * math.tan(ang)
     return math.pi * rad_film ** 2 / (4 * half_w * half_h)
+
+
+# ---- environment-map sampling (rt_set_env_sampling; beyond the reference, see include/rt_abi.h)
+
+def env_plane(rt, w, h, spp=16, c=(0.8, 0.6, 0.4), albedo=(0.25, 0.5, 0.75)):
+    """`bounce` under a constant environment MAP of radiance c (64 x 32 texels) instead of the
+    sky colours.  With environment NEE the estimate per sample is random, but its expectation is
+    still a * c: the NEE term and the MIS-weighted escape split the one bounce."""
+    import numpy as np
+    s = rt.Scene()
+    m = s.add_diffuse_material(albedo, 1.0)
+    s.add_plane(m, (0.0, 1.0, 0.0), 0.0)
+    s.set_environment_map(np.broadcast_to(np.array(c, np.float32), (32, 64, 3)))
+    s.create_scene_bvh()
+    cam = camera(rt, w, h, (0.0, 10.0, -2.0), (0.0, 0.0, 0.5), 30.0)
+    return s, cam, settings(rt, spp, bounces=4), rt.load_reconstruction_kernel("Box"), {
+        "kind": "mean", "value": tuple(a * x for a, x in zip(albedo, c))}
+
+
+def env_sun(rt, w, h, spp=16, lights=False):
+    """A diffuse floor and sphere under a dim sky with a small, very bright sun (128 x 64 map,
+    the sun 4 x 2 texels at 400): the case environment sampling exists for.  `lights` adds a
+    sphere light (the NEE then picks the environment with probability 1/2)."""
+    import numpy as np
+    env = np.full((64, 128, 3), 0.1, np.float32)
+    env[40:42, 70:74] = (400.0, 380.0, 300.0)
+    s = rt.Scene()
+    floor = s.add_diffuse_material((0.6, 0.6, 0.6), 1.0)
+    ball = s.add_diffuse_material((0.2, 0.4, 0.8), 1.0)
+    s.add_plane(floor, (0.0, 1.0, 0.0), 0.0)
+    s.add_sphere(ball, 1.5, rt.translate((0.0, 1.5, 0.0)))
+    if lights:
+        lm = s.add_emissive_material((20.0, 20.0, 18.0))
+        s.add_sphere(lm, 0.5, rt.translate((-3.0, 5.0, 2.0)))
+    s.set_environment_map(env)
+    s.create_scene_bvh()
+    cam = camera(rt, w, h, (0.0, 4.0, -9.0), (0.0, 1.0, 0.0), 40.0)
+    st = settings(rt, spp, bounces=6)
+    return s, cam, st, rt.load_reconstruction_kernel("Box"), None

@@ -52,6 +52,7 @@ def load():
         "oracle_atan2f": (C.c_float, [C.c_float, C.c_float]),
         "oracle_asinf": (C.c_float, [C.c_float]),
         "oracle_set_math_mode": (None, [C.c_int]),
+        "oracle_set_env_sampling": (None, [C.c_int]),
         "oracle_load_filter": (C.c_int, [C.c_char_p, P(abi.FilterCache)]),
         "oracle_postprocess": (None, [P(abi.AccumulationBuffer), P(abi.PostSettings), C.c_uint32, P(C.c_uint32)]),
     }
@@ -118,3 +119,18 @@ def postprocess(accum, post, total_frame_index=0):
     buf = abi.AccumulationBuffer(w, h, 0, accum.ctypes.data_as(C.POINTER(C.c_float)))
     load().oracle_postprocess(C.byref(buf), C.byref(post), total_frame_index, out.ctypes.data_as(C.POINTER(C.c_uint32)))
     return out
+
+
+class env_sampling:
+    """with env_sampling(1): oracle renders with environment-map NEE (oracle_set_env_sampling)."""
+
+    def __init__(self, mode=1):
+        self.mode = mode
+
+    def __enter__(self):
+        load().oracle_set_env_sampling(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        load().oracle_set_env_sampling(0)
+        return False

@@ -24,7 +24,7 @@ def test_every_declared_symbol_is_exported(rt):
     assert len(names) > 40
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.rt_abi_version() == 3
+    assert lib.rt_abi_version() == 4
 
 
 def test_ctypes_table_covers_header(rt):

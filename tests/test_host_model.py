@@ -91,6 +91,7 @@ def test_presets_load(rt, name):
         tris = sum(d.meshes[d.primitives[i].mesh_index].triangle_count for i in range(d.primitive_count)
                    if d.primitives[i].type == 4)
         assert tris >= 250000                  # ~250k-tri multi-mesh scene
+        assert d.mesh_count == 4               # four distinct meshes, not one instanced
     if name in ("c3", "c4", "dragon", "platforms"):
         assert d.skydome_w == 2048 and d.skydome_h == 1024
 
