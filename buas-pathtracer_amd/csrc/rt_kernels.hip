@@ -2707,7 +2707,7 @@ std::vector<float4> top_sequences(const rt_bvh_node* nodes, uint32_t count, uint
 // records are global BVH4 indices (`base` + local); leaves keep the BVH2 packed
 // record (or its index form, mesh-local).  `need` = an upper bound of the stack
 // entries a traversal below this node can hold.  Returns the node's record.
-uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, uint32_t base, std::vector<float4>& out,
+uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, std::vector<float4>& out,
                     uint32_t& need, bool& ok) {
     const uint32_t k = (uint32_t)(out.size() / 8);
     out.resize(out.size() + 8, make_float4(0, 0, 0, 0));
@@ -2738,7 +2738,7 @@ uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, uint32_t b
             ++nchild;
             if (interior(m)) {
                 uint32_t cn = 0;
-                rec = build_bvh4(n, count, m, base, out, cn, ok);
+                rec = build_bvh4(n, count, m, out, cn, ok);
                 deeper = std::max(deeper, cn);
             } else {
                 rec = pack_node(m, c.left_first, c.count, 0);
@@ -2750,8 +2750,8 @@ uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, uint32_t b
     memcpy(&q[7].x, &meta, 4);
     for (int j = 0; j < 8; ++j) out[8*(size_t)k + j] = q[j];
     need = (nchild ? nchild - 1 : 0) + deeper;
-    if (base + k >= (1u << 28)) ok = false;
-    return base + k;
+    if (k >= (1u << 28)) ok = false;
+    return k;                       // out holds every mesh's nodes: k is already the global index
 }
 
 uint32_t tree_depth(const rt_bvh_node* nodes, uint32_t count) {
@@ -3396,7 +3396,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             } else {
                 bool ok = true;
                 uint32_t need = 0;
-                root4[m] = build_bvh4(M.nodes, M.node_count, 0u, (uint32_t)(mnodes4.size() / 8), mnodes4, need, ok);
+                root4[m] = build_bvh4(M.nodes, M.node_count, 0u, mnodes4, need, ok);
                 if (!ok) { set_error("mesh BVH too large for the BVH4 records"); return fail(RT_ERROR_INVALID); }
                 mesh_depth = std::max(mesh_depth, need + 1);
             }
@@ -3489,6 +3489,19 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         if ((err = upload(s, tl.data(), tl.size(), &ds.mnodes))) return fail(err);
     }
     ds.mnodes4 = nullptr;
+    {   // every interior record of the concatenated BVH4s addresses a node that exists
+        const uint32_t n4 = (uint32_t)(mnodes4.size() / 8);
+        bool bad = false;
+        for (uint32_t m = 0; m < d->mesh_count; ++m)
+            bad |= root4[m] < (1u << 28) && root4[m] >= n4 && d->meshes[m].node_count && !d->meshes[m].nodes[0].count;
+        for (size_t k = 0; k < n4 && !bad; ++k)
+            for (int j = 0; j < 4; ++j) {
+                uint32_t r;
+                memcpy(&r, &(&mnodes4[8*k + 6].x)[j], 4);
+                bad |= r != EMPTY4 && r < (1u << 28) && r >= n4;
+            }
+        if (bad) { set_error("internal: mesh BVH4 record out of range"); return fail(RT_ERROR_INVALID); }
+    }
     if (!mnodes4.empty()) {
         mnodes4.resize(mnodes4.size() + FETCH_Q, make_float4(0, 0, 0, 0));
         if ((err = upload(s, mnodes4.data(), mnodes4.size(), &ds.mnodes4))) return fail(err);
@@ -3965,7 +3978,7 @@ int rt_debug_mesh_bvh4(const rt_bvh_node* nodes, uint32_t node_count, float* out
     } else {
         bool ok = true;
         uint32_t need = 0;
-        root = build_bvh4(nodes, node_count, 0u, 0u, q, need, ok);
+        root = build_bvh4(nodes, node_count, 0u, q, need, ok);
         if (!ok) { set_error("BVH too large for the BVH4 records"); return RT_ERROR_INVALID; }
     }
     *out_nodes = (uint32_t)(q.size() / 8);
