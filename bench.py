@@ -55,6 +55,7 @@ CONFIGS = {
     "c2": dict(preset="c2", w=1920, h=1080),
     "c3": dict(preset="c3", w=1920, h=1080),
     "c4": dict(preset="c4", w=1920, h=1080),
+    "c4i": dict(preset="c4i", w=1920, h=1080),     # C4 with one mesh instanced 4 times (the reference's scene)
     "c5": dict(preset="c5", w=3840, h=2160),
 }
 
@@ -129,6 +130,8 @@ def main():
                     help="diagnostic (1 process): render only rank 0's tiles of an N-rank frame, to size the "
                          "per-rank work of the N-GPU strong-scaling run; not a bench line")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--env-sampling", type=int, default=0,
+                    help="1: environment-map NEE (rt_set_env_sampling; beyond the reference's estimator)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     args = ap.parse_args()
 
@@ -161,6 +164,8 @@ def main():
         st.samples_per_pixel = args.spp
     if args.pool:
         rt.lib().rt_set_path_pool(args.pool)
+    if args.env_sampling:
+        rt.set_env_sampling(args.env_sampling)
     dev = rt.DeviceScene(scene, device)
     accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{device}")
     stream = torch.cuda.current_stream(device)
@@ -320,7 +325,8 @@ def main():
             # planes / top-level prologue where they were made
             "traced_rays": [int(traced_all), int(traced_sh_all)],
             "config": {"workload": f"{args.config}: {cfg['preset']} {w}x{h} {st.samples_per_pixel}spp "
-                                   f"depth {st.max_bounce_count}", "width": w, "height": h,
+                                   f"depth {st.max_bounce_count}" + (" env-sampling" if args.env_sampling else ""),
+                       "width": w, "height": h,
                        "spp": st.samples_per_pixel, "max_depth": st.max_bounce_count,
                        "parallelism": (f"tiles%{args.shard_of} (rank 0 only, diagnostic)" if args.shard_of > 1 else f"tiles%{world}" + ("+rccl_reduce" if world > 1 else ""))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
