@@ -1146,7 +1146,10 @@ struct Pool {
     float4* ray_d;       // d.xyz | w: sample offset bits
     float4* thr;         // throughput.xyz | w: vignette
     float4* L;           // total_color.xyz | w: flags bits (bounce 0-7, specular 8, stack_at 9-15)
-    float4* prev_n;      // prev_N.xyz | w: tile-list pixel index p (sample record = s*P + p)
+    // .x: the MIS pdf term of prev_N (RT/integrators.cpp:661-668, dot(prev_N, ray.d) / pi),
+    // computed where the ray's direction is chosen (same operands, same bits), so prev_N
+    // itself is never stored | .y: tile-list pixel index p (sample record = s*P + p)
+    float2* prev_n;
     float2* jitter;
     uint4*  rng;
     float4* hit;         // t | code | tri | v
@@ -1424,7 +1427,7 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
             // deterministic paths: store the sample; k_resolve_tiles / k_resolve gather it
             const uint32_t rel = __float_as_uint(pool.ray_d[slot].w) - pool.rec_pass0;
             const size_t rec = (size_t)(rel < pool.rec_ring ? rel : rel % pool.rec_ring)*fp.pixels +
-                               __float_as_uint(pool.prev_n[slot].w);
+                               __float_as_uint(pool.prev_n[slot].y);
 #if RT_NT_SPLAT
             stnt(&pool.rec_rgbx[rec], make_float4(r.x, r.y, r.z, j.x));     // read again only by the resolve
             stnt(&pool.rec_jy[rec], j.y);
@@ -1571,7 +1574,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
         cast = st.max_bounce_count > 0;
         pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, (RT_DONE_SLIM && !cast) ? vig : __uint_as_float(pack_flags(0, 1, 0)));
-        pool.prev_n[slot] = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(p));
+        pool.prev_n[slot] = make_float2(0.0f, __uint_as_float(p));
         pool.jitter[slot] = make_float2(jx, jy);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         // material_stack[0] = &air: level 0 is never stored; k_shade reads it as sc.air_id
@@ -1770,13 +1773,14 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     // state: the three round trips (state, record, LDS blob) overlap instead of running
     // back to back.  A slot not traced this iteration (~1/6 of the pool) reads 120 B for nothing.
     uint8_t state0 = S_FREE;
-    float4 o4 = {}, d4 = {}, t4 = {}, L4 = {}, pn4 = {}, h4 = {};
+    float4 o4 = {}, d4 = {}, t4 = {}, L4 = {}, h4 = {};
+    float2 pn2 = {};
     uint4 r4 = {};
     float hw = 0.0f;
     if (slot < pool.n) {
         state0 = pool.state[slot];
         o4 = ldnt(&pool.ray_o[slot]); d4 = ldnt(&pool.ray_d[slot]);
-        t4 = ldnt(&pool.thr[slot]); L4 = ldnt(&pool.L[slot]); pn4 = ldnt(&pool.prev_n[slot]);
+        t4 = ldnt(&pool.thr[slot]); L4 = ldnt(&pool.L[slot]); pn2 = ldnt(&pool.prev_n[slot]);
         h4 = ldnt(&pool.hit[slot]); r4 = ldnt(&pool.rng[slot]); hw = ldnt(&pool.hit_w[slot]);
     }
     const DevScene sc = scene_in_lds<IN_LDS>(sc_g, lds_scene);
@@ -1791,7 +1795,8 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         SP_MARK(t_load);
         Rng rng = {r4.x, r4.y, r4.z, r4.w};
         V3 ro = ld3(o4), rd = ld3(d4);
-        V3 thr = ld3(t4), total = ld3(L4), prev_N = ld3(pn4);
+        V3 thr = ld3(t4), total = ld3(L4);
+        float prev_pdf = pn2.x;                      // dot(prev_N, rd) / PI_32 (Pool::prev_n)
         uint32_t flags = __float_as_uint(L4.w);
         uint32_t bounce = flags & 0xFFu, is_spec = (flags >> 8) & 1u;
         int32_t at = (int32_t)((flags >> 9) & 0x7Fu);
@@ -1839,7 +1844,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                 } else if (bounce > 0 && st.use_mis) {
                     float ldsq = t*t;
                     float light_pdf = ldsq / cos_i;
-                    float brdf_pdf = (st.importance_sample_diffuse ? dot(prev_N, rd) / PI_32 : 1.0f / (2.0f*PI_32));
+                    float brdf_pdf = (st.importance_sample_diffuse ? prev_pdf : 1.0f / (2.0f*PI_32));
                     float mis_pdf = light_pdf + brdf_pdf;
                     total = add(total, mul(smul(rcp_cr(mis_pdf), thr), rv3(mt.emission_color)));
                 }
@@ -1972,7 +1977,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                 }
             }
             if (!done) {
-                prev_N = N;
+                if (st.importance_sample_diffuse) prev_pdf = dot(N, rd) / PI_32;   // prev_N = N, and the new ray
                 ++bounce;
                 if (bounce >= st.max_bounce_count) done = true;
             }
@@ -1988,7 +1993,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                     if (st.use_mis) {
                         const float q = sc.light_count > 0 ? 0.5f : 1.0f;
                         float pe = env_pdf(sc, tile, rd);
-                        float bpdf = (st.importance_sample_diffuse ? dot(prev_N, rd) / PI_32 : 1.0f / (2.0f*PI_32));
+                        float bpdf = (st.importance_sample_diffuse ? prev_pdf : 1.0f / (2.0f*PI_32));
                         float den = q*pe + bpdf;
                         wgt = den > 0.0f ? bpdf / den : 0.0f;
                     }
@@ -2024,7 +2029,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         SP_MARK(t_store);
 #if RT_DONE_SLIM
         // A finished path is only splatted: the next k_generate reads L (with the vignette
-        // in .w instead of the flags), the jitter and the .w words of ray_d / prev_n, which
+        // in .w instead of the flags), the jitter, ray_d.w and prev_n.y, which
         // never change.  Its ray, throughput, normal and RNG state are not written back.
         stnt(&pool.L[slot], make_float4(total.x, total.y, total.z,
                                         done ? t4.w : __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
@@ -2032,7 +2037,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             stnt(&pool.ray_o[slot], make_float4(ro.x, ro.y, ro.z, o4.w));
             stnt(&pool.ray_d[slot], make_float4(rd.x, rd.y, rd.z, d4.w));
             stnt(&pool.thr[slot], make_float4(thr.x, thr.y, thr.z, t4.w));
-            stnt(&pool.prev_n[slot], make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w));
+            stnt(&pool.prev_n[slot], make_float2(prev_pdf, pn2.y));
             stnt(&pool.rng[slot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
         }
 #else
@@ -2040,7 +2045,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         stnt(&pool.ray_d[slot], make_float4(rd.x, rd.y, rd.z, d4.w));
         stnt(&pool.thr[slot], make_float4(thr.x, thr.y, thr.z, t4.w));
         stnt(&pool.L[slot], make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
-        stnt(&pool.prev_n[slot], make_float4(prev_N.x, prev_N.y, prev_N.z, pn4.w));
+        stnt(&pool.prev_n[slot], make_float2(prev_pdf, pn2.y));
         stnt(&pool.rng[slot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
 #endif
         SP_ADD(SP_STORE, t_store);
@@ -2827,7 +2832,7 @@ int ensure_pool(Partition& pt, uint32_t n) {
     e |= alloc((void**)&p.ray_d, 16*N);
     e |= alloc((void**)&p.thr, 16*N);
     e |= alloc((void**)&p.L, 16*N);
-    e |= alloc((void**)&p.prev_n, 16*N);
+    e |= alloc((void**)&p.prev_n, 8*N);
     e |= alloc((void**)&p.jitter, 8*N);
     e |= alloc((void**)&p.rng, 16*N);
     e |= alloc((void**)&p.hit, 16*N);
