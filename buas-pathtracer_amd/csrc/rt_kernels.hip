@@ -1153,7 +1153,7 @@ struct Pool {
     float2* jitter;
     uint4*  rng;
     float4* hit;         // t | code | tri | v
-    float*  hit_w;
+    float*  hit_w;       // a mesh hit's w (written by k_trace with the hit; read for mesh hits only)
     uint16_t* mstack;    // [64][n]
     uint8_t*  state;     // S_FREE / S_TRACE / S_DONE per slot
     float4*   ext_rec[2];// extension queues (ping-pong), REC_Q float4 per ray: {o, slot}, {d, t after planes}, {1/d, -}
@@ -1582,7 +1582,6 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         if (cast) {
             pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false, 0u);
             pool.hit[slot] = make_float4(pro.t, __uint_as_float(pro.code), 0.0f, 0.0f);
-            pool.hit_w[slot] = 0.0f;
             enqueue = pro.bvh;
         }
     }
@@ -2022,7 +2021,6 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             SP_MARK(t_cpro);
             cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
             stnt(&pool.hit[slot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
-            stnt(&pool.hit_w[slot], 0.0f);
             enq = cpro.bvh;
             SP_ADD(SP_CPRO, t_cpro);
         }
