@@ -1118,9 +1118,6 @@ RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float
 #ifndef RT_NT_POOL
 #define RT_NT_POOL 1
 #endif
-#ifndef RT_DONE_SLIM
-#define RT_DONE_SLIM 1      // k_shade writes only L (vignette in .w) for a path that finishes
-#endif
 #ifndef RT_NT_SPLAT
 #define RT_NT_SPLAT 1
 #endif
@@ -1140,6 +1137,21 @@ RT_D void stnt(float* p, float v) { __builtin_nontemporal_store(v, p); }
 template <typename T> RT_D T ldnt(const T* p) { return *p; }
 template <typename T> RT_D void stnt(T* p, T v) { *p = v; }
 #endif
+// The path state is double-buffered: k_shade reads a wave's 64 slots of the current buffer
+// and writes the paths that continue, compacted to the front of the same 64 slots of the
+// other buffer (PathOut), and the paths that end into the finished array; the next
+// k_generate fills the wave's remaining slots with new paths.  Every pool array is then
+// written in whole runs (the survivors' prefix, the new paths' suffix) instead of at the
+// scattered slots paths happened to free.  The host swaps the two buffers every iteration.
+struct PathOut {
+    float4 *ray_o, *ray_d, *thr, *L;
+    float2 *prev_n, *jitter;
+    uint4* rng;
+    float4* hit;
+    float* hit_w;
+    uint16_t* mstack;
+    uint8_t* state;
+};
 struct Pool {
     uint32_t n;
     float4* ray_o;       // o.xyz | w: pixel index bits
@@ -1161,8 +1173,17 @@ struct Pool {
     float4*   sh_rec;    // shadow queue, REC_Q float4 per ray: {o, light id}, {d, max_t}, {1/d, -}
     float4*   sh_c;      // contribution.xyz
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
-    uint32_t* free_n;    // [blocks]: slots per BLOCK-slot block free for the next k_generate (k_shade)
+    uint32_t* free_n;    // [blocks]: the block's slots past its survivors, for the next k_generate (k_shade)
     uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
+    PathOut nx;          // the other buffer: k_shade's survivors, k_connect's NEE terms for them
+    // finished paths, per wave of 64 slots compacted from the wave's first entry (k_shade; the next
+    // k_generate splats them, k_connect adds a pending last NEE term): {L, vignette}, {ray_d.w key,
+    // tile-list pixel p, jitter x, jitter y}; fin_w[wave] of them.  free_w[wave]: the wave's
+    // slots past its survivors (free_n[block] is their sum)
+    float4*   fin_L;
+    uint4*    fin_k;
+    uint32_t* fin_w;
+    uint32_t* free_w;
     // This partition's sample records (the deterministic splats): pass s, tile-list pixel p at
     // ((s - rec_pass0) % rec_ring)*P + p.  A ring of rec_ring passes in the streaming splat
     // (k_resolve_tiles frees passes while the frame renders), the partition's whole pass range
@@ -1177,6 +1198,7 @@ struct Pool {
 // appends to come out as runs of consecutive slots (one run per wavefront).
 enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2 };
 constexpr int REC_Q = 3;     // float4 per queued ray record
+constexpr uint32_t SH_FIN = 0x80000000u;   // Pool::sh_slot: the shadow ray's path is in the finished array
 
 // Queues and fetch heads are sharded NSHARD ways (shard = blockIdx % NSHARD, the
 // blocks that share an XCD), each counter on a 128-B line of its own: one word
@@ -1408,26 +1430,21 @@ RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return b
 constexpr int BLOCK = RT_BLOCK;      // slot-ordered kernels (generate / shade)
 constexpr int EV_SLOTS = 8;     // iterations in flight per partition in run_frame (2 chunks of 4)
 
-// The splat of a finished path (RT/raytracer.cpp:469-488): vignette, then the
-// 20-byte sample record k_resolve gathers (splat_filter :187-259 in reference
-// order), or float atomics into the accumulator when the records do not fit.
-// Run by k_generate on the slots the previous iteration finished, before it
-// reuses them.
-RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
+// The splat of a finished path (RT/raytracer.cpp:469-488): vignette (L . vig), then the
+// 20-byte sample record k_resolve gathers (splat_filter :187-259 in reference order), or
+// float atomics into the accumulator when the records do not fit.  Run by k_generate on
+// the finished array k_shade wrote (key: ray_d.w, the sample pass or the list index;
+// p: the tile-list pixel).
+RT_D void splat_sample(const FrameParams& fp, const Pool& pool, V3 L, float vig, float2 j, uint32_t key, uint32_t p) {
     {
-        const float4 L = pool.L[slot];
-        const float vig = RT_DONE_SLIM ? L.w : pool.thr[slot].w;     // k_shade / k_generate put it in L.w
-        const float2 j = pool.jitter[slot];
-        V3 r = muls(ld3(L), vig);
+        V3 r = muls(L, vig);
         if (fp.list_xy) {
-            const uint32_t k = __float_as_uint(pool.ray_d[slot].w);
-            float* o = fp.list_out + 5*(size_t)k;
+            float* o = fp.list_out + 5*(size_t)key;
             o[0] = r.x; o[1] = r.y; o[2] = r.z; o[3] = j.x; o[4] = j.y;
         } else if (pool.rec_rgbx) {
             // deterministic paths: store the sample; k_resolve_tiles / k_resolve gather it
-            const uint32_t rel = __float_as_uint(pool.ray_d[slot].w) - pool.rec_pass0;
-            const size_t rec = (size_t)(rel < pool.rec_ring ? rel : rel % pool.rec_ring)*fp.pixels +
-                               __float_as_uint(pool.prev_n[slot].y);
+            const uint32_t rel = key - pool.rec_pass0;
+            const size_t rec = (size_t)(rel < pool.rec_ring ? rel : rel % pool.rec_ring)*fp.pixels + p;
 #if RT_NT_SPLAT
             stnt(&pool.rec_rgbx[rec], make_float4(r.x, r.y, r.z, j.x));     // read again only by the resolve
             stnt(&pool.rec_jy[rec], j.y);
@@ -1436,8 +1453,8 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
             pool.rec_jy[rec] = j.y;
 #endif
         } else if (fp.cache_size) {
-            const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
-            const int64_t x = pixel % fp.w, y = pixel / fp.w;
+            const uint32_t xy = fp.pix_xy[p];
+            const int64_t x = xy & 0xFFFFu, y = xy >> 16;
             const int64_t ks = fp.kernel_size;
             const float kscale = (float)(fp.cache_size - 1) / (float)ks;
             int64_t x0 = x - ks, x1 = x + ks + 1, y0 = y - ks, y1 = y + ks + 1;
@@ -1460,8 +1477,8 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, uint32_t slot) {
                 }
             }
         } else {
-            const uint32_t pixel = __float_as_uint(pool.ray_o[slot].w);
-            float* dst = reinterpret_cast<float*>(fp.accum + pixel);
+            const uint32_t xy = fp.pix_xy[p];
+            float* dst = reinterpret_cast<float*>(fp.accum + (size_t)(xy >> 16)*fp.w + (xy & 0xFFFFu));
             unsafeAtomicAdd(dst + 0, r.x);
             unsafeAtomicAdd(dst + 1, r.y);
             unsafeAtomicAdd(dst + 2, r.z);
@@ -1493,34 +1510,36 @@ constexpr uint32_t GEN_LDS_Q_SCALE = RT_GEN_LDS_SCENE ? 16u : 0u;   // dynamic L
 // k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
 __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                     Counters* cnt, int cur) {
-    __shared__ uint32_t agg[BLOCK / 64 + 1];
-    // Free slots claim consecutive sample numbers in slot order: the block's first
-    // claim is the scan of the free counts k_bookkeep made (no atomics).  The block's
-    // free slots are handed to its first nfree threads (slot order kept), so the waves
-    // past them skip the ray setup entirely (about 2/3 of the pool is busy at any time).
-    __shared__ uint16_t freelist[BLOCK];
-    const uint32_t own = blockIdx.x*blockDim.x + threadIdx.x;
-    const uint8_t own_state = own < pool.n ? pool.state[own] : (uint8_t)S_TRACE;
-    if (own_state == S_DONE) {                   // the previous iteration finished this path: splat it
-        splat_sample(fp, pool, own);
-        pool.state[own] = S_FREE;                // a claim below may reuse the slot (ordered by the barrier)
+    // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
+    // splat them.  Their NEE contributions from k_connect are in by now.
+    const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
+    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
+    if (lane < pool.fin_w[wbase]) {
+        const float4 fl = ldnt(&pool.fin_L[slot]);
+        const uint4 fk = ldnt(&pool.fin_k[slot]);
+        splat_sample(fp, pool, ld3(fl), fl.w, make_float2(__uint_as_float(fk.z), __uint_as_float(fk.w)), fk.x, fk.y);
     }
-    // No sample left for this block to claim (the frame's drain): splat only, no scene copy
-    if ((unsigned long long)pool.claim_base[blockIdx.x] >= remaining_samples(cnt)) return;
+    // Each wave's survivors fill its first slots; the rest take new paths, claiming consecutive
+    // sample numbers in slot order from the scan of the free counts k_bookkeep made (no atomics):
+    // the block's first claim, the free slots of the block's earlier waves, the lane's rank.
+    const uint32_t first = 64u - pool.free_w[wbase];
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += pool.free_w[wbase - wave + w];
+    const bool want = lane >= first;
+    const uint32_t claim = pool.claim_base[blockIdx.x] + before + (lane - first);
+    // No sample left for this block to claim (the frame's drain): its free slots go idle
+    if ((unsigned long long)pool.claim_base[blockIdx.x] >= remaining_samples(cnt)) {
+        if (want) pool.state[slot] = S_FREE;
+        return;
+    }
 #if RT_GEN_LDS_SCENE
     const DevScene sc = scene_in_lds(sc_g, lds_scene);
 #else
     const DevScene& sc = sc_g;       // nothing generate reads lives in the LDS copy (see RT_GEN_LDS_SCENE)
 #endif
-    const bool own_free = own_state != S_TRACE;
-    uint32_t nfree;
-    const uint32_t rank = block_rank<BLOCK>(own_free, agg, &nfree);
-    if (own_free) freelist[rank] = (uint16_t)threadIdx.x;
-    __syncthreads();
-    const bool want = threadIdx.x < nfree;
-    const uint32_t slot = blockIdx.x*blockDim.x + (want ? (uint32_t)freelist[threadIdx.x] : threadIdx.x);
-    const uint32_t claim = pool.claim_base[blockIdx.x] + threadIdx.x;
     const bool active = want && (unsigned long long)claim < remaining_samples(cnt);
+    if (want && !active) pool.state[slot] = S_FREE;
     bool enqueue = false, cast = false;
     V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
     Prologue pro = {};
@@ -1573,7 +1592,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
         pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
         cast = st.max_bounce_count > 0;
-        pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, (RT_DONE_SLIM && !cast) ? vig : __uint_as_float(pack_flags(0, 1, 0)));
+        pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, !cast ? vig : __uint_as_float(pack_flags(0, 1, 0)));
         pool.prev_n[slot] = make_float2(0.0f, __uint_as_float(p));
         pool.jitter[slot] = make_float2(jx, jy);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
@@ -1674,9 +1693,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             if (!tr.occluded) {
                 const uint32_t slot = pool.sh_slot[item];
                 const float4 c = ldnt(&pool.sh_c[item]);
-                float4 L = ldnt(&pool.L[slot]);
+                float4* const dst = (slot & SH_FIN) ? &pool.fin_L[slot & ~SH_FIN] : &pool.nx.L[slot];
+                float4 L = ldnt(dst);
                 L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;   // total_color += ... (:768)
-                stnt(&pool.L[slot], L);
+                stnt(dst, L);
             }
         } else if (tr.code != RT_HIT_MISS) {                  // a BVH hit; else k_shade's plane result stands
             const uint32_t slot = item;                       // the path's slot (from the record)
@@ -1790,6 +1810,11 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     V3 sh_o = {0, 0, 0}, sh_d = {0, 0, 0}, sh_c = {0, 0, 0};
     float sh_t = 0.0f;
     uint32_t sh_light = 0;
+    uint32_t nslot = 0;                                                // a survivor's slot in pool.nx
+    // finished-array entries (see the tail): the slots k_generate made finished, then the paths
+    // that end here
+    const bool made_fin = slot < pool.n && state0 == S_DONE;
+    const unsigned long long made_fin_mask = __ballot(made_fin);
     if (valid) {
         SP_MARK(t_load);
         Rng rng = {r4.x, r4.y, r4.z, r4.w};
@@ -1875,7 +1900,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                         if (at > 0) --at;
                     } else if (at < 63) {
                         ++at;
-                        pool.mstack[(size_t)at*pool.n + slot] = (uint16_t)mt_id;
+                        pool.mstack[(size_t)at*pool.n + slot] = (uint16_t)mt_id;   // moved with the path below
                     }
                     V3 fd = add(smul(eta, rd), muls(N, (eta*cos_i - cos_t)));
                     ro = add(I, muls(fd, EPSILON)); rd = fd;
@@ -2017,46 +2042,65 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         }
         cont = !done;
         nro = ro; nrd = rd;
+        // The wave's paths that continue go, in slot order, to the front of its 64 slots in the
+        // other buffer (pool.nx): a ballot, no barrier.  The next k_generate fills the rest.
+        const unsigned long long smask = __ballot(cont);
+        nslot = (slot & ~63u) + (uint32_t)__popcll(smask & ((1ull << __lane_id()) - 1ull));
         if (cont) {                                        // next bounce's intersect_scene: planes + top level here
             SP_MARK(t_cpro);
             cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
-            stnt(&pool.hit[slot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
+            stnt(&pool.nx.hit[nslot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
             enq = cpro.bvh;
             SP_ADD(SP_CPRO, t_cpro);
         }
         SP_MARK(t_store);
-#if RT_DONE_SLIM
-        // A finished path is only splatted: the next k_generate reads L (with the vignette
-        // in .w instead of the flags), the jitter, ray_d.w and prev_n.y, which
-        // never change.  Its ray, throughput, normal and RNG state are not written back.
-        stnt(&pool.L[slot], make_float4(total.x, total.y, total.z,
-                                        done ? t4.w : __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
-        if (!done) {
-            stnt(&pool.ray_o[slot], make_float4(ro.x, ro.y, ro.z, o4.w));
-            stnt(&pool.ray_d[slot], make_float4(rd.x, rd.y, rd.z, d4.w));
-            stnt(&pool.thr[slot], make_float4(thr.x, thr.y, thr.z, t4.w));
-            stnt(&pool.prev_n[slot], make_float2(prev_pdf, pn2.y));
-            stnt(&pool.rng[slot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
+        // A path that ends here goes to the wave's finished array; its state is not written back.
+        const unsigned long long fm = made_fin_mask | __ballot(done);
+        if (done) {
+            const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
+            const float2 j = ldnt(&pool.jitter[slot]);
+            stnt(&pool.fin_L[fidx], make_float4(total.x, total.y, total.z, t4.w));
+            stnt(&pool.fin_k[fidx], make_uint4(__float_as_uint(d4.w), __float_as_uint(pn2.y),
+                                               __float_as_uint(j.x), __float_as_uint(j.y)));
         }
-#else
-        stnt(&pool.ray_o[slot], make_float4(ro.x, ro.y, ro.z, o4.w));
-        stnt(&pool.ray_d[slot], make_float4(rd.x, rd.y, rd.z, d4.w));
-        stnt(&pool.thr[slot], make_float4(thr.x, thr.y, thr.z, t4.w));
-        stnt(&pool.L[slot], make_float4(total.x, total.y, total.z, __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
-        stnt(&pool.prev_n[slot], make_float2(prev_pdf, pn2.y));
-        stnt(&pool.rng[slot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
-#endif
+        if (cont) {
+            stnt(&pool.nx.ray_o[nslot], make_float4(ro.x, ro.y, ro.z, o4.w));
+            stnt(&pool.nx.ray_d[nslot], make_float4(rd.x, rd.y, rd.z, d4.w));
+            stnt(&pool.nx.thr[nslot], make_float4(thr.x, thr.y, thr.z, t4.w));
+            stnt(&pool.nx.L[nslot], make_float4(total.x, total.y, total.z,
+                                                __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
+            stnt(&pool.nx.prev_n[nslot], make_float2(prev_pdf, pn2.y));
+            stnt(&pool.nx.jitter[nslot], ldnt(&pool.jitter[slot]));
+            stnt(&pool.nx.rng[nslot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
+            pool.nx.state[nslot] = S_TRACE;
+            // the material stack moves with the path (levels 1..at; level 0 is the implicit air)
+            for (int32_t lv = 1; lv <= at; ++lv)
+                pool.nx.mstack[(size_t)lv*pool.n + nslot] = pool.mstack[(size_t)lv*pool.n + slot];
+        }
         SP_ADD(SP_STORE, t_store);
     }
     SP_MARK(t_tail);
     const int nxt = cur ^ 1;
     const uint32_t shard = blockIdx.x % NSHARD;
-    // slots the next k_generate may claim (scanned by k_bookkeep): finished now or idle; and
-    // the finished ones it must splat first (the host's termination test waits for them)
-    const bool idle = slot < pool.n && !valid;
-    const bool unsplat = done || (idle && state0 == S_DONE);
+    // The wave's paths that end here (or were made finished: max_bounce_count 0) go to the front of
+    // its 64 entries of the finished array, which the next k_generate splats before it fills the
+    // wave's slots past the survivors with new paths (the host's termination test waits for them).
+    const bool fin = done || made_fin;
+    const unsigned long long fmask = __ballot(fin);
+    const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fmask & ((1ull << __lane_id()) - 1ull));
+    if (made_fin) {                                 // L = 0 with the vignette in .w (k_generate)
+        const float2 j = ldnt(&pool.jitter[slot]);
+        stnt(&pool.fin_L[fidx], pool.L[slot]);
+        stnt(&pool.fin_k[fidx], make_uint4(__float_as_uint(d4.w), __float_as_uint(pn2.y),
+                                           __float_as_uint(j.x), __float_as_uint(j.y)));
+    }
+    const unsigned long long cmask = __ballot(cont);
+    if (__lane_id() == 0) {
+        pool.free_w[slot >> 6] = 64u - (uint32_t)__popcll(cmask);
+        pool.fin_w[slot >> 6] = (uint32_t)__popcll(fmask);
+    }
     __shared__ uint32_t tally[(BLOCK / 64 + 2)*6];
-    const bool tp[6] = {enq, shadow, cont, cast_shadow, unsplat, done || idle};
+    const bool tp[6] = {enq, shadow, cont, cast_shadow, fin, slot < pool.n && !cont};
     uint32_t* const tc[6] = {&cnt->ext_count[nxt][shard][0], &cnt->shadow_count[shard][0], &cnt->alive[shard][0],
                              &cnt->cast[1][shard][0], &cnt->unsplat[shard][0], nullptr};
     uint32_t tpos[6], ttot[6];
@@ -2064,20 +2108,20 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const uint32_t pos = tpos[0];
     if (enq) {
         float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + pos);
-        stnt(&q[0], make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot)));
+        stnt(&q[0], make_float4(nro.x, nro.y, nro.z, __uint_as_float(nslot)));
         stnt(&q[1], make_float4(nrd.x, nrd.y, nrd.z, cpro.t));
         stnt(&q[2], make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, __uint_as_float(cpro.mlist)));
     }
     const uint32_t spos = shard*pool.shard_cap + tpos[1];
     if (shadow) {
-        pool.sh_slot[spos] = slot;
+        // the NEE term goes to the survivor's L in pool.nx, or to the finished entry
+        pool.sh_slot[spos] = cont ? nslot : (SH_FIN | fidx);
         float4* q = pool.sh_rec + REC_Q*(size_t)spos;
         stnt(&q[0], make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light)));
         stnt(&q[1], make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t));
         stnt(&q[2], make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist)));
         stnt(&pool.sh_c[spos], make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f));
     }
-    if (done) pool.state[slot] = S_DONE;
     if (threadIdx.x == 0) pool.free_n[blockIdx.x] = ttot[5];
 #if RT_SHADE_PROF
     SP_ADD(SP_TAIL, t_tail);
@@ -2826,6 +2870,21 @@ int ensure_pool(Partition& pt, uint32_t n) {
     p.shard_cap = (uint32_t)cap;
     e |= alloc((void**)&p.free_n, 4*nblocks);
     e |= alloc((void**)&p.claim_base, 4*nblocks);
+    e |= alloc((void**)&p.fin_w, 4*(N / 64));
+    e |= alloc((void**)&p.free_w, 4*(N / 64));
+    e |= alloc((void**)&p.fin_L, 16*N);
+    e |= alloc((void**)&p.fin_k, 16*N);
+    e |= alloc((void**)&p.nx.ray_o, 16*N);
+    e |= alloc((void**)&p.nx.ray_d, 16*N);
+    e |= alloc((void**)&p.nx.thr, 16*N);
+    e |= alloc((void**)&p.nx.L, 16*N);
+    e |= alloc((void**)&p.nx.prev_n, 8*N);
+    e |= alloc((void**)&p.nx.jitter, 8*N);
+    e |= alloc((void**)&p.nx.rng, 16*N);
+    e |= alloc((void**)&p.nx.hit, 16*N);
+    e |= alloc((void**)&p.nx.hit_w, 4*N);
+    e |= alloc((void**)&p.nx.mstack, 2*64*N);
+    e |= alloc((void**)&p.nx.state, N);
     e |= alloc((void**)&p.ray_o, 16*N);
     e |= alloc((void**)&p.ray_d, 16*N);
     e |= alloc((void**)&p.thr, 16*N);
@@ -2845,6 +2904,17 @@ int ensure_pool(Partition& pt, uint32_t n) {
     if (e) { free_pool(pt); return RT_ERROR_OUT_OF_MEMORY; }
     p.n = n;
     return RT_OK;
+}
+
+// The pool as the kernels of an iteration see it: buffer `par` current, the other one PathOut.
+Pool pool_view(const Pool& p, int par) {
+    if (!par) return p;
+    Pool v = p;
+    std::swap(v.ray_o, v.nx.ray_o); std::swap(v.ray_d, v.nx.ray_d); std::swap(v.thr, v.nx.thr);
+    std::swap(v.L, v.nx.L); std::swap(v.prev_n, v.nx.prev_n); std::swap(v.jitter, v.nx.jitter);
+    std::swap(v.rng, v.nx.rng); std::swap(v.hit, v.nx.hit); std::swap(v.hit_w, v.nx.hit_w);
+    std::swap(v.mstack, v.nx.mstack); std::swap(v.state, v.nx.state);
+    return v;
 }
 
 int check_inputs(const rt_settings* st, const rt_filter_cache* f) {
@@ -2985,6 +3055,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + 2, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
+        HIP_OK(hipMemsetAsync(pt.pool.fin_w, 0, 4ull*N / 64, r.stream));
+        HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_w, 64, N / 64, r.stream));
         k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{});
         if (prof && !pt.events) {
             for (auto& e : pt.ev) HIP_OK(hipEventCreate(&e));
@@ -3026,30 +3098,31 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         const int slot = (int)(r.iters % EV_SLOTS);
         auto b = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
         auto e = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
+        const Pool pv = pool_view(pt.pool, r.cur);        // the path buffers swap every iteration
         b(RT_KERNEL_GENERATE);
-        k_generate<<<r.grid, BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+        k_generate<<<r.grid, BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
-        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
-        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
+        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         if (env) {
-            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
-            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
+            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         } else if (s->ds.blob_q) {
-            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         } else {
-            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pt.pool, pt.cnt, r.cur);
+            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
-        else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pt.pool, pt.cnt, r.cur, pt.spill, diag);
+        if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
+        else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_CONNECT);
         const bool res = stream_splat && plan;
-        k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pt.pool, r.grid, r.cur, BK_ITER, plan_of(k, res ? 1u : 0u));
+        k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pv, r.grid, r.cur, BK_ITER, plan_of(k, res ? 1u : 0u));
         r.res_ev[slot] = res && ((prof >> RT_KERNEL_RESOLVE) & 1u);
         if (res) {                       // the passes the bookkeep found complete, if enough of them
             b(RT_KERNEL_RESOLVE);
-            launch_resolve_tiles(sp, fp, pt.pool, pt.cnt, r.dst, q);
+            launch_resolve_tiles(sp, fp, pv, pt.cnt, r.dst, q);
             e(RT_KERNEL_RESOLVE);
         }
         ++r.iters;
