@@ -2042,17 +2042,16 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         }
         cont = !done;
         nro = ro; nrd = rd;
+        if (cont) {                                        // next bounce's intersect_scene: planes + top level here
+            SP_MARK(t_cpro);
+            cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
+            enq = cpro.bvh;
+            SP_ADD(SP_CPRO, t_cpro);
+        }
         // The wave's paths that continue go, in slot order, to the front of its 64 slots in the
         // other buffer (pool.nx): a ballot, no barrier.  The next k_generate fills the rest.
         const unsigned long long smask = __ballot(cont);
         nslot = (slot & ~63u) + (uint32_t)__popcll(smask & ((1ull << __lane_id()) - 1ull));
-        if (cont) {                                        // next bounce's intersect_scene: planes + top level here
-            SP_MARK(t_cpro);
-            cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
-            stnt(&pool.nx.hit[nslot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
-            enq = cpro.bvh;
-            SP_ADD(SP_CPRO, t_cpro);
-        }
         SP_MARK(t_store);
         // A path that ends here goes to the wave's finished array; its state is not written back.
         const unsigned long long fm = made_fin_mask | __ballot(done);
@@ -2064,6 +2063,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                                                __float_as_uint(j.x), __float_as_uint(j.y)));
         }
         if (cont) {
+            stnt(&pool.nx.hit[nslot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
             stnt(&pool.nx.ray_o[nslot], make_float4(ro.x, ro.y, ro.z, o4.w));
             stnt(&pool.nx.ray_d[nslot], make_float4(rd.x, rd.y, rd.z, d4.w));
             stnt(&pool.nx.thr[nslot], make_float4(thr.x, thr.y, thr.z, t4.w));
