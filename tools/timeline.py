@@ -3,8 +3,10 @@
 
 usage: tools/timeline.py gpurun_out/prof_<TAG>/run_kernel_trace.csv [--bucket-ms 5]
 
-Takes the bench's second frame (frames start with k_pixel_map), prints the mean number of
-kernels in flight per bucket, the time per kernel, and where the last resolve runs.
+Takes the bench's second frame (a frame ends with k_combine_partials, the streaming splat's last
+launch; the frame layout, k_pixel_map included, is built once per scene), prints the mean number
+of kernels in flight per bucket, the time per kernel, per-partition iteration counts (one k_bookkeep
+per iteration) and where the last resolve runs.
 """
 import argparse
 import csv
@@ -16,10 +18,11 @@ def main():
     ap.add_argument("--bucket-ms", type=float, default=5.0)
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace)) if r["Kernel_Name"].startswith(("k_", "void k_"))]
-    ri = [i for i, r in enumerate(rows) if "k_pixel_map" in r["Kernel_Name"]]
-    if len(ri) < 2:
-        raise SystemExit("need two frames (two k_pixel_map launches) in the trace")
-    fr = rows[ri[1]:ri[2]] if len(ri) > 2 else rows[ri[0]:ri[1]]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ends = [i for i, r in enumerate(rows) if "k_combine_partials" in r["Kernel_Name"]]
+    if len(ends) < 2:
+        raise SystemExit("need two frames (two k_combine_partials launches) in the trace")
+    fr = rows[ends[0] + 1:ends[1] + 1]
     t0 = min(int(r["Start_Timestamp"]) for r in fr)
     t1 = max(int(r["End_Timestamp"]) for r in fr)
     bucket = int(a.bucket_ms * 1e6)
