@@ -2492,10 +2492,21 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
     // (all loads in flight), then a wave scan by shuffles and one barrier for the 16 wave totals.
     // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
     // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
+    // Up to BK_EMAX entries per thread (pools up to 32k blocks, 8.4M paths) are loaded at once into
+    // registers, all in flight, and the claims are written from them; a loop covers larger pools.
+    constexpr uint32_t BK_EMAX = 32;
     const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
     const uint32_t lo = t*E, hi = min(lo + E, nblocks);
     uint32_t sum = 0;
-    for (uint32_t i = lo; i < hi; ++i) sum += pool.free_n[i];
+    uint32_t v[BK_EMAX];
+    if (E <= BK_EMAX) {
+#pragma unroll
+        for (uint32_t j = 0; j < BK_EMAX; ++j) v[j] = lo + j < hi ? pool.free_n[lo + j] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < BK_EMAX; ++j) sum += v[j];
+    } else {
+        for (uint32_t i = lo; i < hi; ++i) sum += pool.free_n[i];
+    }
     const uint32_t lane = t & 63u, wave = t >> 6;
     uint32_t incl = sum;
 #pragma unroll
@@ -2508,10 +2519,16 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += sc[w];
     uint32_t run = before + incl - sum;
-    for (uint32_t i = lo; i < hi; ++i) {
-        const uint32_t v = pool.free_n[i];
-        pool.claim_base[i] = run;
-        run += v;
+    if (E <= BK_EMAX) {
+#pragma unroll
+        for (uint32_t j = 0; j < BK_EMAX; ++j)
+            if (lo + j < hi) { pool.claim_base[lo + j] = run; run += v[j]; }
+    } else {
+        for (uint32_t i = lo; i < hi; ++i) {
+            const uint32_t x = pool.free_n[i];
+            pool.claim_base[i] = run;
+            run += x;
+        }
     }
     if (t == BK_THREADS - 1) carry = run;
     __syncthreads();
