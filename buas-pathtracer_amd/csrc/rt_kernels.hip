@@ -1124,15 +1124,20 @@ RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float
 typedef float nt_f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
 typedef float nt_f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t nt_u2 __attribute__((ext_vector_type(2)));
 #if RT_NT_POOL
 RT_D float4 ldnt(const float4* p) { const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p)); return make_float4(v.x, v.y, v.z, v.w); }
 RT_D uint4 ldnt(const uint4* p) { const nt_u4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_u4*>(p)); return make_uint4(v.x, v.y, v.z, v.w); }
 RT_D float2 ldnt(const float2* p) { const nt_f2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f2*>(p)); return make_float2(v.x, v.y); }
 RT_D float ldnt(const float* p) { return __builtin_nontemporal_load(p); }
+RT_D uint2 ldnt(const uint2* p) { const nt_u2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_u2*>(p)); return make_uint2(v.x, v.y); }
+RT_D uint32_t ldnt(const uint32_t* p) { return __builtin_nontemporal_load(p); }
 RT_D void stnt(float4* p, float4 v) { const nt_f4 t = {v.x, v.y, v.z, v.w}; __builtin_nontemporal_store(t, reinterpret_cast<nt_f4*>(p)); }
 RT_D void stnt(uint4* p, uint4 v) { const nt_u4 t = {v.x, v.y, v.z, v.w}; __builtin_nontemporal_store(t, reinterpret_cast<nt_u4*>(p)); }
 RT_D void stnt(float2* p, float2 v) { const nt_f2 t = {v.x, v.y}; __builtin_nontemporal_store(t, reinterpret_cast<nt_f2*>(p)); }
 RT_D void stnt(float* p, float v) { __builtin_nontemporal_store(v, p); }
+RT_D void stnt(uint2* p, uint2 v) { const nt_u2 t = {v.x, v.y}; __builtin_nontemporal_store(t, reinterpret_cast<nt_u2*>(p)); }
+RT_D void stnt(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
 #else
 template <typename T> RT_D T ldnt(const T* p) { return *p; }
 template <typename T> RT_D void stnt(T* p, T v) { *p = v; }
@@ -1145,7 +1150,7 @@ template <typename T> RT_D void stnt(T* p, T v) { *p = v; }
 // scattered slots paths happened to free.  The host swaps the two buffers every iteration.
 struct PathOut {
     float4 *ray_o, *ray_d, *thr, *L;
-    float2 *prev_n, *jitter;
+    float2* prev_n;
     uint4* rng;
     float4* hit;
     float* hit_w;
@@ -1162,7 +1167,6 @@ struct Pool {
     // computed where the ray's direction is chosen (same operands, same bits), so prev_N
     // itself is never stored | .y: tile-list pixel index p (sample record = s*P + p)
     float2* prev_n;
-    float2* jitter;
     uint4*  rng;
     float4* hit;         // t | code | tri | v
     float*  hit_w;       // a mesh hit's w (written by k_trace with the hit; read for mesh hits only)
@@ -1178,10 +1182,11 @@ struct Pool {
     PathOut nx;          // the other buffer: k_shade's survivors, k_connect's NEE terms for them
     // finished paths, per wave of 64 slots compacted from the wave's first entry (k_shade; the next
     // k_generate splats them, k_connect adds a pending last NEE term): {L, vignette}, {ray_d.w key,
-    // tile-list pixel p, jitter x, jitter y}; fin_w[wave] of them.  free_w[wave]: the wave's
-    // slots past its survivors (free_n[block] is their sum)
+    // tile-list pixel p}, ray_o.w pixel; fin_w[wave] of them.  free_w[wave]: the wave's slots past
+    // its survivors (free_n[block] is their sum).  The AA jitter is recomputed (sample_jitter).
     float4*   fin_L;
-    uint4*    fin_k;
+    uint2*    fin_k;
+    uint32_t* fin_px;
     uint32_t* fin_w;
     uint32_t* free_w;
     // This partition's sample records (the deterministic splats): pass s, tile-list pixel p at
@@ -1499,6 +1504,19 @@ __global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out
         out[base + local] = (min_x + local % tw) | ((min_y + local / tw) << 16);
 }
 
+// The AA jitter of sample s of pixel (x, y): render_tile's first sampler draw (RT/raytracer.cpp:
+// 431-435).  The sample's RandomSeries is seeded from its key and this draw comes first, so the
+// jitter is a function of the key: the splat recomputes it instead of carrying it with the path.
+RT_D V2 sample_jitter(const DevScene& sc, const rt_settings& st, const FrameParams& fp, uint32_t x, uint32_t y,
+                      uint32_t s) {
+    const uint32_t canonical = fp.frame_count + s;
+    const uint32_t tile = (y / fp.tile_h)*fp.tcx + (x / fp.tile_w);
+    Rng rng = random_seed(sample_seed(fp.total_frame_index, fp.frame_count, tile, y*fp.w + x, canonical));
+    const SamplerState ss = {x, y, canonical, st.sampling_strategy};
+    const V2 aa = sample_2d(sc, ss, rng, S_AA, 0);
+    return {aa.x - 0.5f, aa.y - 0.5f};
+}
+
 // k_generate reads only the sampler tables and the ray prologue's tables, which stay in HBM
 // (RT_LDS_STRATA = 0) and are read through the scalar cache (RT_PROLOGUE_SCALAR): a block
 // needs no LDS copy of the scene, so it skips that copy, its barrier and its LDS footprint.
@@ -1517,8 +1535,11 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
     if (lane < pool.fin_w[wbase]) {
         const float4 fl = ldnt(&pool.fin_L[slot]);
-        const uint4 fk = ldnt(&pool.fin_k[slot]);
-        splat_sample(fp, pool, ld3(fl), fl.w, make_float2(__uint_as_float(fk.z), __uint_as_float(fk.w)), fk.x, fk.y);
+        const uint2 fk = ldnt(&pool.fin_k[slot]);
+        const uint32_t pixel = ldnt(&pool.fin_px[slot]);
+        const uint32_t s = fp.list_xy ? fp.list_s[fk.x] : fk.x;
+        const V2 j = sample_jitter(sc_g, st, fp, pixel % fp.w, pixel / fp.w, s);
+        splat_sample(fp, pool, ld3(fl), fl.w, make_float2(j.x, j.y), fk.x, fk.y);
     }
     // Each wave's survivors fill its first slots; the rest take new paths, claiming consecutive
     // sample numbers in slot order from the scan of the free counts k_bookkeep made (no atomics):
@@ -1594,7 +1615,6 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         cast = st.max_bounce_count > 0;
         pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, !cast ? vig : __uint_as_float(pack_flags(0, 1, 0)));
         pool.prev_n[slot] = make_float2(0.0f, __uint_as_float(p));
-        pool.jitter[slot] = make_float2(jx, jy);
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         // material_stack[0] = &air: level 0 is never stored; k_shade reads it as sc.air_id
         pool.state[slot] = cast ? S_TRACE : S_DONE;      // max_bounce_count == 0: nothing to trace
@@ -1761,7 +1781,9 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 }
 
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
-#ifdef RT_SHADE_WAVES
+#if defined(RT_SHADE_MAX_WAVES)
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(1, RT_SHADE_MAX_WAVES)))
+#elif defined(RT_SHADE_WAVES)
 #define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WAVES)))
 #else
 #define RT_SHADE_ATTR
@@ -2057,10 +2079,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         const unsigned long long fm = made_fin_mask | __ballot(done);
         if (done) {
             const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
-            const float2 j = ldnt(&pool.jitter[slot]);
             stnt(&pool.fin_L[fidx], make_float4(total.x, total.y, total.z, t4.w));
-            stnt(&pool.fin_k[fidx], make_uint4(__float_as_uint(d4.w), __float_as_uint(pn2.y),
-                                               __float_as_uint(j.x), __float_as_uint(j.y)));
+            stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(d4.w), __float_as_uint(pn2.y)));
+            stnt(&pool.fin_px[fidx], __float_as_uint(o4.w));
         }
         if (cont) {
             stnt(&pool.nx.hit[nslot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
@@ -2070,7 +2091,6 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             stnt(&pool.nx.L[nslot], make_float4(total.x, total.y, total.z,
                                                 __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
             stnt(&pool.nx.prev_n[nslot], make_float2(prev_pdf, pn2.y));
-            stnt(&pool.nx.jitter[nslot], ldnt(&pool.jitter[slot]));
             stnt(&pool.nx.rng[nslot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
             pool.nx.state[nslot] = S_TRACE;
             // the material stack moves with the path (levels 1..at; level 0 is the implicit air)
@@ -2089,10 +2109,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const unsigned long long fmask = __ballot(fin);
     const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fmask & ((1ull << __lane_id()) - 1ull));
     if (made_fin) {                                 // L = 0 with the vignette in .w (k_generate)
-        const float2 j = ldnt(&pool.jitter[slot]);
         stnt(&pool.fin_L[fidx], pool.L[slot]);
-        stnt(&pool.fin_k[fidx], make_uint4(__float_as_uint(d4.w), __float_as_uint(pn2.y),
-                                           __float_as_uint(j.x), __float_as_uint(j.y)));
+        stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(d4.w), __float_as_uint(pn2.y)));
+        stnt(&pool.fin_px[fidx], __float_as_uint(o4.w));
     }
     const unsigned long long cmask = __ballot(cont);
     if (__lane_id() == 0) {
@@ -2890,13 +2909,13 @@ int ensure_pool(Partition& pt, uint32_t n) {
     e |= alloc((void**)&p.fin_w, 4*(N / 64));
     e |= alloc((void**)&p.free_w, 4*(N / 64));
     e |= alloc((void**)&p.fin_L, 16*N);
-    e |= alloc((void**)&p.fin_k, 16*N);
+    e |= alloc((void**)&p.fin_k, 8*N);
+    e |= alloc((void**)&p.fin_px, 4*N);
     e |= alloc((void**)&p.nx.ray_o, 16*N);
     e |= alloc((void**)&p.nx.ray_d, 16*N);
     e |= alloc((void**)&p.nx.thr, 16*N);
     e |= alloc((void**)&p.nx.L, 16*N);
     e |= alloc((void**)&p.nx.prev_n, 8*N);
-    e |= alloc((void**)&p.nx.jitter, 8*N);
     e |= alloc((void**)&p.nx.rng, 16*N);
     e |= alloc((void**)&p.nx.hit, 16*N);
     e |= alloc((void**)&p.nx.hit_w, 4*N);
@@ -2907,7 +2926,6 @@ int ensure_pool(Partition& pt, uint32_t n) {
     e |= alloc((void**)&p.thr, 16*N);
     e |= alloc((void**)&p.L, 16*N);
     e |= alloc((void**)&p.prev_n, 8*N);
-    e |= alloc((void**)&p.jitter, 8*N);
     e |= alloc((void**)&p.rng, 16*N);
     e |= alloc((void**)&p.hit, 16*N);
     e |= alloc((void**)&p.hit_w, 4*N);
@@ -2928,7 +2946,7 @@ Pool pool_view(const Pool& p, int par) {
     if (!par) return p;
     Pool v = p;
     std::swap(v.ray_o, v.nx.ray_o); std::swap(v.ray_d, v.nx.ray_d); std::swap(v.thr, v.nx.thr);
-    std::swap(v.L, v.nx.L); std::swap(v.prev_n, v.nx.prev_n); std::swap(v.jitter, v.nx.jitter);
+    std::swap(v.L, v.nx.L); std::swap(v.prev_n, v.nx.prev_n);
     std::swap(v.rng, v.nx.rng); std::swap(v.hit, v.nx.hit); std::swap(v.hit_w, v.nx.hit_w);
     std::swap(v.mstack, v.nx.mstack); std::swap(v.state, v.nx.state);
     return v;
