@@ -2692,7 +2692,8 @@ struct rt_scene {
     size_t tiles_cap = 0;
     int32_t* d_tile_base = nullptr;
     size_t tile_base_cap = 0;
-    uint32_t trace_grid = 0;        // persistent k_trace blocks
+    uint32_t trace_grid = 0;        // persistent k_trace blocks (extend)
+    uint32_t connect_grid = 0;      // persistent k_trace<true> blocks (<= trace_grid: the spill area)
     float4* d_samp = nullptr;       // per-sample records for the deterministic splat
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
@@ -3149,8 +3150,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (s->ds.listed_only) k_trace<true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
-        else k_trace<true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
+        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
+        else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_CONNECT);
         const bool res = stream_splat && plan;
         k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pv, r.grid, r.cur, BK_ITER, plan_of(k, res ? 1u : 0u));
@@ -3673,7 +3674,15 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         // area is sized from the result.
         int grid_pct = 75;
         if (const char* e = getenv("RT_TRACE_GRID_PCT")) grid_pct = std::max(1, atoi(e));
-        s->trace_grid = std::max(1u, (uint32_t)((unsigned long long)s->trace_grid*(unsigned)grid_pct / 100ull));
+        const uint32_t full = s->trace_grid;
+        s->trace_grid = std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)grid_pct / 100ull));
+        // Shadow-ray launches carry a quarter of the extension rays (~0.8 per lane of a 75 % grid):
+        // a 25 % grid does them as fast and leaves the registers to the other partitions' kernels
+        // (C3: +0.6 %, 2 pairs; 40 / 55 % between).
+        int connect_pct = 25;
+        if (const char* e = getenv("RT_CONNECT_GRID_PCT")) connect_pct = std::max(1, atoi(e));
+        s->connect_grid = std::min(s->trace_grid,
+                                   std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)connect_pct / 100ull)));
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
