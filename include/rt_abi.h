@@ -352,7 +352,7 @@ int rt_set_profiling(int enable);
 int rt_set_profiling_stages(uint32_t mask);
 
 /* Size of the in-flight path pool per partition (paths resident in HBM); 0 = default:
- * an eighth of the partition's samples, clamped to [2^21, 3 x 2^21]. */
+ * a fifth of the partition's samples, clamped to [2^21, 3 x 2^21]. */
 int rt_set_path_pool(uint32_t paths);
 
 /* How samples reach the accumulation buffer (splat_filter, RT/raytracer.cpp:187-259).
