@@ -2447,7 +2447,10 @@ __global__ void __launch_bounds__(256) k_combine_partials(float4* accum, const f
 // limit moves to keep the ring from overwriting passes not yet resolved.
 enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
 struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life; };
-constexpr int BK_THREADS = 1024;
+#ifndef RT_BK_THREADS
+#define RT_BK_THREADS 1024
+#endif
+constexpr int BK_THREADS = RT_BK_THREADS;
 __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
                                                          ResPlan plan) {
     __shared__ uint32_t sc[BK_THREADS];
@@ -2513,7 +2516,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
     // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
     // Up to BK_EMAX entries per thread (pools up to 32k blocks, 8.4M paths) are loaded at once into
     // registers, all in flight, and the claims are written from them; a loop covers larger pools.
-    constexpr uint32_t BK_EMAX = 32;
+    constexpr uint32_t BK_EMAX = 32*(1024 / BK_THREADS);
     const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
     const uint32_t lo = t*E, hi = min(lo + E, nblocks);
     uint32_t sum = 0;
