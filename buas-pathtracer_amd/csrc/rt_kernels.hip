@@ -1221,7 +1221,8 @@ struct Counters {
     uint32_t pending;               // paths queued for the next iteration (host termination test)
     uint32_t pending_splat;         // finished paths the next k_generate splats (host termination test)
     uint32_t cancel;
-    uint32_t pad;
+    uint32_t done;                  // every sample claimed, traced and splatted (k_bookkeep); the launches
+                                    // still queued behind it (drain mode) exit at once
     unsigned long long step_stats[2][8];   // RT_STEP_STATS builds: see k_trace
     uint32_t max_steps[2];          // diagnostics: longest traversal (steps) per kind
     float    worst_ray[2][8];       // o.xyz, d.xyz, max_t, steps of a ray above the step threshold
@@ -1804,7 +1805,7 @@ __device__ unsigned long long g_shade_prof[SP_N + 1];
 // ENV: rt_set_env_sampling on, the scene has an environment map and NEE is on
 template <bool IN_LDS, bool ENV>
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
-                                                 Counters* cnt, int cur) {
+                                                 Counters* cnt, int cur, int sparse) {
 #if RT_SHADE_PROF
     unsigned long long prof[SP_N] = {};
     SP_MARK(t_start);
@@ -1813,16 +1814,27 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     // The slot's state and path record are loaded before the scene copy, whatever the
     // state: the three round trips (state, record, LDS blob) overlap instead of running
     // back to back.  A slot not traced this iteration (~1/6 of the pool) reads 120 B for nothing.
+    // In the frame's drain (`sparse`: nothing left to claim, most slots idle) the record is read
+    // only for the slots that hold a path, after their state; a partition already done exits.
     uint8_t state0 = S_FREE;
     float4 o4 = {}, d4 = {}, t4 = {}, L4 = {}, h4 = {};
     float2 pn2 = {};
     uint4 r4 = {};
     float hw = 0.0f;
-    if (slot < pool.n) {
-        state0 = pool.state[slot];
+    auto load_path = [&]() {
         o4 = ldnt(&pool.ray_o[slot]); d4 = ldnt(&pool.ray_d[slot]);
         t4 = ldnt(&pool.thr[slot]); L4 = ldnt(&pool.L[slot]); pn2 = ldnt(&pool.prev_n[slot]);
         h4 = ldnt(&pool.hit[slot]); r4 = ldnt(&pool.rng[slot]); hw = ldnt(&pool.hit_w[slot]);
+    };
+    if (sparse) {
+        if (cnt->done) return;                                          // uniform: every block reads it
+        if (slot < pool.n) {
+            state0 = pool.state[slot];
+            if (state0 != S_FREE) load_path();
+        }
+    } else if (slot < pool.n) {
+        state0 = pool.state[slot];
+        load_path();
     }
     const DevScene sc = scene_in_lds<IN_LDS>(sc_g, lds_scene);
     const bool valid = slot < pool.n && state0 == S_TRACE;             // traced this iteration
@@ -2464,8 +2476,11 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         }
         return;
     }
+    __shared__ uint32_t skip;
     if (t == 0) {
-        if (phase == BK_ITER) {
+        skip = phase == BK_ITER && cnt->done;           // the partition finished in an earlier iteration
+        if (skip) cnt->res_from = cnt->res_to = 0;      // its last passes are resolved already
+        if (phase == BK_ITER && !skip) {
             const unsigned long long rem = remaining_samples(cnt);
             cnt->next_sample += ((unsigned long long)cnt->gen_free < rem ? (unsigned long long)cnt->gen_free : rem);
             uint32_t ext = 0, sh = 0, pend = 0, tq = 0, ts = 0, ps = 0;
@@ -2491,11 +2506,14 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             cnt->traced_rays[1] += ts;
             cnt->pending = pend;
             cnt->pending_splat = ps;
+            // nothing left to claim, trace or splat: every record is in the ring
+            const bool complete = cnt->next_sample >= cnt->total_samples && pend == 0 && ps == 0;
+            if (complete) cnt->done = 1;
             const uint32_t it = cnt->iter++;
             cnt->hist[it & 127u] = cnt->next_sample;
             if (plan.mode) {
                 const unsigned long long done = it >= plan.life ? cnt->hist[(it - plan.life) & 127u] : cnt->start_sample;
-                const uint32_t done_pass = (uint32_t)(done / plan.P);
+                const uint32_t done_pass = complete ? plan.pass1 : (uint32_t)(done / plan.P);
                 const uint32_t from = cnt->res_cursor;
                 cnt->res_from = cnt->res_to = 0;
                 if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
@@ -2510,6 +2528,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         carry = 0;
     }
     __syncthreads();
+    if (skip) return;
     // exclusive scan of free_n: thread t owns the contiguous entries [t*E, t*E + E), sums them
     // (all loads in flight), then a wave scan by shuffles and one barrier for the 16 wave totals.
     // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
@@ -3048,7 +3067,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(s->start_ev, stream));
-    struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live; int final_buf;
+    struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live, drain; int final_buf;
                  uint64_t chunk_first[2]; int chunk_n[2]; uint32_t pass0, pass1, ring; float4* dst;
                  bool res_ev[EV_SLOTS]; };
     Run run[MAX_PARTITIONS] = {};
@@ -3143,6 +3162,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         auto b = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
         auto e = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
         const Pool pv = pool_view(pt.pool, r.cur);        // the path buffers swap every iteration
+        const int sparse = r.drain ? 1 : 0;
         b(RT_KERNEL_GENERATE);
         k_generate<<<r.grid, BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
@@ -3150,18 +3170,20 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         if (env) {
-            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
-            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
+            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
+            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
         } else if (s->ds.blob_q) {
-            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
+            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
         } else {
-            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
+            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
         if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
         else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
         e(RT_KERNEL_CONNECT);
-        const bool res = stream_splat && plan;
+        // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
+        // partition complete resolves its last passes at once, without waiting for the host
+        const bool res = stream_splat && (plan || r.drain);
         k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pv, r.grid, r.cur, BK_ITER, plan_of(k, res ? 1u : 0u));
         r.res_ev[slot] = res && ((prof >> RT_KERNEL_RESOLVE) & 1u);
         if (res) {                       // the passes the bookkeep found complete, if enough of them
@@ -3222,6 +3244,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             harvest(k, b);
             ++r.consumed;
             const Counters& c = s->part[k].cnt_host[b];
+            if (c.next_sample >= c.total_samples) r.drain = true;     // the chunks enqueued from now on
             if (c.next_sample >= c.total_samples && c.pending == 0 && c.pending_splat == 0) {
                 r.live = false; r.final_buf = b; --live;       // its chunk still in flight finds nothing to do
                 int err = finish(k);
@@ -3873,10 +3896,13 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         if (sp.mode == RT_SPLAT_EXACT && (double)total*20.0 > budget) sp.mode = RT_SPLAT_STREAM;
         if (sp.mode == RT_SPLAT_STREAM && ks > 12) sp.mode = (double)total*20.0 <= budget ? RT_SPLAT_EXACT : RT_SPLAT_ATOMIC;
         if (sp.mode == RT_SPLAT_STREAM) {
-            // a resolve every ~32M samples; the ring holds the passes not yet resolved: the chunk,
-            // the claims of the iterations a path can live (about 5 pool fills) and slack
+            // a resolve every ~32M samples, and at least four per partition (a small shard, e.g. one
+            // rank's eighth of a frame, would otherwise resolve all its passes after its drain); the
+            // ring holds the passes not yet resolved: the chunk, the claims of the iterations a path
+            // can live (about 5 pool fills) and slack
             const uint32_t per_part = (spp + shape.nparts - 1) / shape.nparts;
-            sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull), per_part);
+            sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull),
+                                                               std::max(1u, per_part / 4));
             if (const char* e = getenv("RT_SPLAT_CHUNK")) sp.chunk = std::max(1, atoi(e));
             const unsigned long long lag = (5ull*shape.pool_n + fp.pixels - 1) / fp.pixels;
             sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, per_part);
