@@ -1223,6 +1223,11 @@ struct Counters {
     uint32_t cancel;
     uint32_t done;                  // every sample claimed, traced and splatted (k_bookkeep); the launches
                                     // still queued behind it (drain mode) exit at once
+    uint32_t fused;                 // nothing left to claim and few paths alive (k_bookkeep): the next
+                                    // iteration launched with the drain kernels runs every remaining
+                                    // path to its end in k_drain; its extend / shade / connect exit
+    uint32_t drain_count[NSHARD][LINE_WORDS];   // k_drain_list: live slots per shard (in Pool::sh_slot)
+    uint32_t drain_fetch[NSHARD][LINE_WORDS];   // k_drain: items handed out per shard
     unsigned long long step_stats[2][8];   // RT_STEP_STATS builds: see k_trace
     uint32_t max_steps[2];          // diagnostics: longest traversal (steps) per kind
     float    worst_ray[2][8];       // o.xyz, d.xyz, max_t, steps of a ray above the step threshold
@@ -1675,7 +1680,9 @@ constexpr int STEPS_PER_REFILL_SHADOW = RT_STEPS_PER_REFILL_SHADOW;
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
 template <bool OCC, bool LST>
-__global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag) {
+__global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag,
+                                                              int fuse) {
+    if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
 #ifdef RT_TRACE_PRIO
     // trace waves are latency bound and issue little; shade waves sharing the SIMD are
     // issue bound: let a trace wave's next load go out first
@@ -1802,10 +1809,230 @@ __device__ unsigned long long g_shade_prof[SP_N + 1];
 #define SP_MARK(v)
 #define SP_ADD(i, a)
 #endif
+// One bounce of advanced_integrator (RT/integrators.cpp:612-815) for a path whose closest hit
+// is h: emission / MIS, Beer absorption, Fresnel, reflect / refract / diffuse with NEE (the
+// shadow ray is returned, not traced) and Russian roulette.  Shared by k_shade (one bounce per
+// launch) and k_drain (a path's remaining bounces in one launch), so both compute the same bits.
+// The material stack lives at pool.mstack[level*n + slot].  Returns true when the path ends.
+#if RT_SHADE_PROF
+#define SP_PARAM , unsigned long long* prof
+#define SP_PASS , prof
+#else
+#define SP_PARAM
+#define SP_PASS
+#endif
+template <bool ENV>
+RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerState& ss, const Pool& pool,
+                       uint32_t slot, const Hit& h, V3& ro, V3& rd, V3& thr, V3& total, float& prev_pdf,
+                       uint32_t& bounce, uint32_t& is_spec, int32_t& at, Rng& rng, bool& cast_shadow,
+                       V3& sh_o, V3& sh_d, V3& sh_c, float& sh_t, uint32_t& sh_light SP_PARAM) {
+    bool done = false;
+    if (h.code != RT_HIT_MISS) {
+        SP_MARK(t_geom);
+        V3 I, N;
+        uint32_t surf_id;
+        Ray ray; ray.o = ro; ray.d = rd;
+        hit_geometry(sc, ray, h, I, N, surf_id);
+        float t = h.t;
+        float cos_i = -dot(rd, N);
+        bool inside = (cos_i < 0.0f);
+        uint32_t mi_id, mt_id;
+        if (inside) {
+            mi_id = surf_id;
+            const int32_t lv = at - 1 > 0 ? at - 1 : 0;
+            mt_id = lv ? pool.mstack[(size_t)lv*pool.n + slot] : sc.air_id;     // level 0 = air
+            cos_i = -cos_i;
+            N = neg(N);
+        } else {
+            mi_id = at ? pool.mstack[(size_t)at*pool.n + slot] : sc.air_id;
+            mt_id = surf_id;
+        }
+        const rt_material mi = sc.materials[mi_id];
+        const rt_material mt = sc.materials[mt_id];
+        SP_ADD(SP_GEOM, t_geom);
+        if (mi.is_participating_medium) {                                  // Beer :640-649
+            V3 ab = {d_expf(-mi.absorb.x*t), d_expf(-mi.absorb.y*t), d_expf(-mi.absorb.z*t)};
+            thr = mul(thr, ab);
+        }
+        if (mt.flags & RT_MATERIAL_EMISSIVE) {                             // :651-670
+            SP_MARK(t_emis);
+            bool allow = (!st.next_event_estimation ||
+                          ((st.caustics || (bounce < 2)) && is_spec));
+            if (allow) {
+                total = add(total, mul(thr, rv3(mt.emission_color)));
+            } else if (bounce > 0 && st.use_mis) {
+                float ldsq = t*t;
+                float light_pdf = ldsq / cos_i;
+                float brdf_pdf = (st.importance_sample_diffuse ? prev_pdf : 1.0f / (2.0f*PI_32));
+                float mis_pdf = light_pdf + brdf_pdf;
+                total = add(total, mul(smul(rcp_cr(mis_pdf), thr), rv3(mt.emission_color)));
+            }
+            done = true;
+            SP_ADD(SP_EMIS, t_emis);
+        } else {
+            SP_MARK(t_fres);
+            float eta_i = mi.ior, eta_t = mt.ior;
+            float eta = eta_i / eta_t;
+            float cos_t;
+            float refl = fresnel_dielectric(cos_i, eta_i, eta_t, eta, cos_t);
+            float reflect_test = sample_1d(sc, ss, rng, S_Reflectance, bounce);
+            refl = lerpf_(refl, 1.0f, mt.metallic);
+            is_spec = 1;
+            SP_ADD(SP_FRES, t_fres);
+            if (reflect_test < refl) {                                      // reflect :684-696
+                SP_MARK(t_refl);
+                V3 nd = reflect(rd, N);
+                if (mt.roughness > 0.0f) {
+                    V3 rs = random_in_unit_sphere(rng);
+                    nd = normalize(add(smul(1.0f + EPSILON, nd), smul(mt.roughness, rs)));
+                }
+                ro = add(I, smul(EPSILON, nd)); rd = nd;
+                thr = mul(thr, lerp3(v3s(1.0f), rv3(mt.albedo), mt.metallic));
+                SP_ADD(SP_REFL, t_refl);
+            } else if (mt.is_participating_medium) {                       // refract :698-717
+                SP_MARK(t_refr);
+                if (inside) {
+                    if (at > 0) --at;
+                } else if (at < 63) {
+                    ++at;
+                    pool.mstack[(size_t)at*pool.n + slot] = (uint16_t)mt_id;   // moved with the path below
+                }
+                V3 fd = add(smul(eta, rd), muls(N, (eta*cos_i - cos_t)));
+                ro = add(I, muls(fd, EPSILON)); rd = fd;
+                SP_ADD(SP_REFR, t_refr);
+            } else {                                                        // diffuse :718-790
+                SP_MARK(t_nee);
+                is_spec = 0;
+                V3 albedo = evaluate_material(mt, I);
+                V3 brdf = smul(1.0f / PI_32, albedo);
+                if (st.next_event_estimation && (sc.light_count > 0 || ENV)) {      // NEE :738-771
+                    float lps = sample_1d(sc, ss, rng, S_LightSelection, bounce);
+                    // ENV: the environment is picked with probability q (1 without lights)
+                    const float q = sc.light_count > 0 ? 0.5f : 1.0f;
+                    const bool pick_env = ENV && lps < q;
+                    if (ENV) lps = pick_env ? lps / q : (lps - q) / (1.0f - q);
+                    float lrp = 0.0f;
+                    uint32_t lid = pick_env ? 0u : pick_random_light(sc, st, lps, I, lrp);
+                    if (ENV) lrp = lrp*(1.0f - q);
+                    V2 s2 = sample_2d(sc, ss, rng, S_DirectLighting, bounce);
+                    if (pick_env) {
+                        V3 Lv = env_direction(sc, lps, s2);
+                        float ndl = dot(N, Lv);
+                        if (ndl > 0.0f) {
+                            uint32_t tile;
+                            V3 Le = sky_env(sc, Lv, tile);
+                            float pe = env_pdf(sc, tile, Lv);
+                            if (pe > 0.0f) {
+                                float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
+                                float pdf = st.use_mis ? q*pe + bpdf : q*pe;
+                                sh_c = mul(mul(muls(thr, ndl / pdf), brdf), Le);
+                                sh_o = add(I, muls(Lv, EPSILON));
+                                sh_d = Lv;
+                                sh_t = FLT_MAX_;
+                                sh_light = 0;                   // the null primitive: nothing ignored
+                                cast_shadow = true;
+                            }
+                        }
+                    } else {
+                        // random_point_on_light (:199-228), sphere lights
+                        const rt_primitive light = sc.prims[lid];
+                        const M34 lf = load_m34(&sc.fwd[light.transform_index]);
+                        V3 towards = normalize(sub(translation(lf), I));
+                        if (light.type == RT_PRIMITIVE_SPHERE) {
+                            float rad = light.p[0];
+                            V3 Nl = map_to_hemisphere(neg(towards), s2);
+                            V3 pw = xform(lf, muls(Nl, rad), 1.0f);
+                            V3 Lv = sub(pw, I);
+                            float dsq = length_sq(Lv);
+                            float dist = __builtin_sqrtf(dsq);
+                            Lv = divs(Lv, dist);
+                            float A = 2.0f*PI_32*rad*rad;
+                            float ndl = dot(N, Lv);
+                            float nndl = -dot(Nl, Lv);
+                            if (ndl > 0.0f && nndl > 0.0f) {
+                                float sa = (nndl * A) / dsq;
+                                float pdf;
+                                if (st.use_mis) {
+                                    float lpdf = rcp_cr(sa);
+                                    float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
+                                    pdf = lpdf + bpdf;
+                                } else {
+                                    pdf = rcp_cr(sa);
+                                }
+                                pdf *= lrp;
+                                sh_c = mul(mul(muls(thr, dot(N, Lv) / pdf), brdf),
+                                           rv3(sc.materials[light.material_id].emission_color));
+                                sh_o = add(I, muls(Lv, EPSILON));
+                                sh_d = Lv;
+                                sh_t = dist - 2*EPSILON;
+                                sh_light = lid;
+                                cast_shadow = true;                 // traced below, lanes reconverged
+                            }
+                        }
+                    }
+                }
+                SP_ADD(SP_NEE, t_nee);
+                SP_MARK(t_ind);
+                V2 s2 = sample_2d(sc, ss, rng, S_IndirectLighting, bounce); // indirect :777-789
+                V3 R;
+                if (st.importance_sample_diffuse) {
+                    R = map_to_cosine_weighted_hemisphere(N, s2);
+                    thr = muls(thr, PI_32);
+                } else {
+                    R = map_to_hemisphere(N, s2);
+                    thr = muls(thr, 2.0f*PI_32*dot(N, R));
+                }
+                thr = mul(thr, brdf);
+                ro = add(I, muls(N, EPSILON)); rd = R;
+                SP_ADD(SP_IND, t_ind);
+            }
+            if (st.russian_roulette && !is_spec) {                          // RR :801-811
+                SP_MARK(t_rr);
+                float p = clampf_(max3(thr), 0.1f, 0.9f);
+                float e = sample_1d(sc, ss, rng, S_Roulette, bounce);
+                if (e > p) done = true;
+                else thr = muls(thr, rcp_cr(p));
+                SP_ADD(SP_RR, t_rr);
+            }
+        }
+        if (!done) {
+            if (st.importance_sample_diffuse) prev_pdf = dot(N, rd) / PI_32;   // prev_N = N, and the new ray
+            ++bounce;
+            if (bounce >= st.max_bounce_count) done = true;
+        }
+    } else {
+        SP_MARK(t_sky);
+        if (ENV) {
+            // a path leaving a diffuse vertex (which sampled the environment in its NEE):
+            // balance heuristic against that pdf; without MIS the NEE alone carries it
+            uint32_t tile;
+            V3 Le = sky_env(sc, rd, tile);
+            if (!is_spec) {
+                float wgt = 0.0f;
+                if (st.use_mis) {
+                    const float q = sc.light_count > 0 ? 0.5f : 1.0f;
+                    float pe = env_pdf(sc, tile, rd);
+                    float bpdf = (st.importance_sample_diffuse ? prev_pdf : 1.0f / (2.0f*PI_32));
+                    float den = q*pe + bpdf;
+                    wgt = den > 0.0f ? bpdf / den : 0.0f;
+                }
+                Le = smul(wgt, Le);
+            }
+            total = add(total, mul(thr, Le));
+        } else {
+            total = add(total, mul(thr, sample_sky(sc, rd)));             // miss :812-815
+        }
+        done = true;
+        SP_ADD(SP_SKY, t_sky);
+    }
+    return done;
+}
+
 // ENV: rt_set_env_sampling on, the scene has an environment map and NEE is on
 template <bool IN_LDS, bool ENV>
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
-                                                 Counters* cnt, int cur, int sparse) {
+                                                 Counters* cnt, int cur, int sparse, int fuse) {
+    if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
 #if RT_SHADE_PROF
     unsigned long long prof[SP_N] = {};
     SP_MARK(t_start);
@@ -1865,205 +2092,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         SamplerState ss = {px, py, canonical, st.sampling_strategy};
         Hit h;
         h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = hw;
-        Ray ray; ray.o = ro; ray.d = rd;
         SP_ADD(SP_LOAD, t_load);
-        if (h.code != RT_HIT_MISS) {
-            SP_MARK(t_geom);
-            V3 I, N;
-            uint32_t surf_id;
-            hit_geometry(sc, ray, h, I, N, surf_id);
-            float t = h.t;
-            float cos_i = -dot(rd, N);
-            bool inside = (cos_i < 0.0f);
-            uint32_t mi_id, mt_id;
-            if (inside) {
-                mi_id = surf_id;
-                const int32_t lv = at - 1 > 0 ? at - 1 : 0;
-                mt_id = lv ? pool.mstack[(size_t)lv*pool.n + slot] : sc.air_id;     // level 0 = air
-                cos_i = -cos_i;
-                N = neg(N);
-            } else {
-                mi_id = at ? pool.mstack[(size_t)at*pool.n + slot] : sc.air_id;
-                mt_id = surf_id;
-            }
-            const rt_material mi = sc.materials[mi_id];
-            const rt_material mt = sc.materials[mt_id];
-            SP_ADD(SP_GEOM, t_geom);
-            if (mi.is_participating_medium) {                                  // Beer :640-649
-                V3 ab = {d_expf(-mi.absorb.x*t), d_expf(-mi.absorb.y*t), d_expf(-mi.absorb.z*t)};
-                thr = mul(thr, ab);
-            }
-            if (mt.flags & RT_MATERIAL_EMISSIVE) {                             // :651-670
-                SP_MARK(t_emis);
-                bool allow = (!st.next_event_estimation ||
-                              ((st.caustics || (bounce < 2)) && is_spec));
-                if (allow) {
-                    total = add(total, mul(thr, rv3(mt.emission_color)));
-                } else if (bounce > 0 && st.use_mis) {
-                    float ldsq = t*t;
-                    float light_pdf = ldsq / cos_i;
-                    float brdf_pdf = (st.importance_sample_diffuse ? prev_pdf : 1.0f / (2.0f*PI_32));
-                    float mis_pdf = light_pdf + brdf_pdf;
-                    total = add(total, mul(smul(rcp_cr(mis_pdf), thr), rv3(mt.emission_color)));
-                }
-                done = true;
-                SP_ADD(SP_EMIS, t_emis);
-            } else {
-                SP_MARK(t_fres);
-                float eta_i = mi.ior, eta_t = mt.ior;
-                float eta = eta_i / eta_t;
-                float cos_t;
-                float refl = fresnel_dielectric(cos_i, eta_i, eta_t, eta, cos_t);
-                float reflect_test = sample_1d(sc, ss, rng, S_Reflectance, bounce);
-                refl = lerpf_(refl, 1.0f, mt.metallic);
-                is_spec = 1;
-                SP_ADD(SP_FRES, t_fres);
-                if (reflect_test < refl) {                                      // reflect :684-696
-                    SP_MARK(t_refl);
-                    V3 nd = reflect(rd, N);
-                    if (mt.roughness > 0.0f) {
-                        V3 rs = random_in_unit_sphere(rng);
-                        nd = normalize(add(smul(1.0f + EPSILON, nd), smul(mt.roughness, rs)));
-                    }
-                    ro = add(I, smul(EPSILON, nd)); rd = nd;
-                    thr = mul(thr, lerp3(v3s(1.0f), rv3(mt.albedo), mt.metallic));
-                    SP_ADD(SP_REFL, t_refl);
-                } else if (mt.is_participating_medium) {                       // refract :698-717
-                    SP_MARK(t_refr);
-                    if (inside) {
-                        if (at > 0) --at;
-                    } else if (at < 63) {
-                        ++at;
-                        pool.mstack[(size_t)at*pool.n + slot] = (uint16_t)mt_id;   // moved with the path below
-                    }
-                    V3 fd = add(smul(eta, rd), muls(N, (eta*cos_i - cos_t)));
-                    ro = add(I, muls(fd, EPSILON)); rd = fd;
-                    SP_ADD(SP_REFR, t_refr);
-                } else {                                                        // diffuse :718-790
-                    SP_MARK(t_nee);
-                    is_spec = 0;
-                    V3 albedo = evaluate_material(mt, I);
-                    V3 brdf = smul(1.0f / PI_32, albedo);
-                    if (st.next_event_estimation && (sc.light_count > 0 || ENV)) {      // NEE :738-771
-                        float lps = sample_1d(sc, ss, rng, S_LightSelection, bounce);
-                        // ENV: the environment is picked with probability q (1 without lights)
-                        const float q = sc.light_count > 0 ? 0.5f : 1.0f;
-                        const bool pick_env = ENV && lps < q;
-                        if (ENV) lps = pick_env ? lps / q : (lps - q) / (1.0f - q);
-                        float lrp = 0.0f;
-                        uint32_t lid = pick_env ? 0u : pick_random_light(sc, st, lps, I, lrp);
-                        if (ENV) lrp = lrp*(1.0f - q);
-                        V2 s2 = sample_2d(sc, ss, rng, S_DirectLighting, bounce);
-                        if (pick_env) {
-                            V3 Lv = env_direction(sc, lps, s2);
-                            float ndl = dot(N, Lv);
-                            if (ndl > 0.0f) {
-                                uint32_t tile;
-                                V3 Le = sky_env(sc, Lv, tile);
-                                float pe = env_pdf(sc, tile, Lv);
-                                if (pe > 0.0f) {
-                                    float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
-                                    float pdf = st.use_mis ? q*pe + bpdf : q*pe;
-                                    sh_c = mul(mul(muls(thr, ndl / pdf), brdf), Le);
-                                    sh_o = add(I, muls(Lv, EPSILON));
-                                    sh_d = Lv;
-                                    sh_t = FLT_MAX_;
-                                    sh_light = 0;                   // the null primitive: nothing ignored
-                                    cast_shadow = true;
-                                }
-                            }
-                        } else {
-                            // random_point_on_light (:199-228), sphere lights
-                            const rt_primitive light = sc.prims[lid];
-                            const M34 lf = load_m34(&sc.fwd[light.transform_index]);
-                            V3 towards = normalize(sub(translation(lf), I));
-                            if (light.type == RT_PRIMITIVE_SPHERE) {
-                                float rad = light.p[0];
-                                V3 Nl = map_to_hemisphere(neg(towards), s2);
-                                V3 pw = xform(lf, muls(Nl, rad), 1.0f);
-                                V3 Lv = sub(pw, I);
-                                float dsq = length_sq(Lv);
-                                float dist = __builtin_sqrtf(dsq);
-                                Lv = divs(Lv, dist);
-                                float A = 2.0f*PI_32*rad*rad;
-                                float ndl = dot(N, Lv);
-                                float nndl = -dot(Nl, Lv);
-                                if (ndl > 0.0f && nndl > 0.0f) {
-                                    float sa = (nndl * A) / dsq;
-                                    float pdf;
-                                    if (st.use_mis) {
-                                        float lpdf = rcp_cr(sa);
-                                        float bpdf = (st.importance_sample_diffuse ? ndl / PI_32 : 1.0f / (2.0f*PI_32));
-                                        pdf = lpdf + bpdf;
-                                    } else {
-                                        pdf = rcp_cr(sa);
-                                    }
-                                    pdf *= lrp;
-                                    sh_c = mul(mul(muls(thr, dot(N, Lv) / pdf), brdf),
-                                               rv3(sc.materials[light.material_id].emission_color));
-                                    sh_o = add(I, muls(Lv, EPSILON));
-                                    sh_d = Lv;
-                                    sh_t = dist - 2*EPSILON;
-                                    sh_light = lid;
-                                    cast_shadow = true;                 // traced below, lanes reconverged
-                                }
-                            }
-                        }
-                    }
-                    SP_ADD(SP_NEE, t_nee);
-                    SP_MARK(t_ind);
-                    V2 s2 = sample_2d(sc, ss, rng, S_IndirectLighting, bounce); // indirect :777-789
-                    V3 R;
-                    if (st.importance_sample_diffuse) {
-                        R = map_to_cosine_weighted_hemisphere(N, s2);
-                        thr = muls(thr, PI_32);
-                    } else {
-                        R = map_to_hemisphere(N, s2);
-                        thr = muls(thr, 2.0f*PI_32*dot(N, R));
-                    }
-                    thr = mul(thr, brdf);
-                    ro = add(I, muls(N, EPSILON)); rd = R;
-                    SP_ADD(SP_IND, t_ind);
-                }
-                if (st.russian_roulette && !is_spec) {                          // RR :801-811
-                    SP_MARK(t_rr);
-                    float p = clampf_(max3(thr), 0.1f, 0.9f);
-                    float e = sample_1d(sc, ss, rng, S_Roulette, bounce);
-                    if (e > p) done = true;
-                    else thr = muls(thr, rcp_cr(p));
-                    SP_ADD(SP_RR, t_rr);
-                }
-            }
-            if (!done) {
-                if (st.importance_sample_diffuse) prev_pdf = dot(N, rd) / PI_32;   // prev_N = N, and the new ray
-                ++bounce;
-                if (bounce >= st.max_bounce_count) done = true;
-            }
-        } else {
-            SP_MARK(t_sky);
-            if (ENV) {
-                // a path leaving a diffuse vertex (which sampled the environment in its NEE):
-                // balance heuristic against that pdf; without MIS the NEE alone carries it
-                uint32_t tile;
-                V3 Le = sky_env(sc, rd, tile);
-                if (!is_spec) {
-                    float wgt = 0.0f;
-                    if (st.use_mis) {
-                        const float q = sc.light_count > 0 ? 0.5f : 1.0f;
-                        float pe = env_pdf(sc, tile, rd);
-                        float bpdf = (st.importance_sample_diffuse ? prev_pdf : 1.0f / (2.0f*PI_32));
-                        float den = q*pe + bpdf;
-                        wgt = den > 0.0f ? bpdf / den : 0.0f;
-                    }
-                    Le = smul(wgt, Le);
-                }
-                total = add(total, mul(thr, Le));
-            } else {
-                total = add(total, mul(thr, sample_sky(sc, rd)));             // miss :812-815
-            }
-            done = true;
-            SP_ADD(SP_SKY, t_sky);
-        }
+        done = shade_bounce<ENV>(sc, st, ss, pool, slot, h, ro, rd, thr, total, prev_pdf, bounce, is_spec, at, rng,
+                                 cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light SP_PASS);
         if (cast_shadow) {
             // intersect_shadow_ray (:756): planes and the top level here; only rays that meet
             // a mesh are queued for k_trace<true>.  Nothing else adds to total_color after the
@@ -2167,6 +2198,185 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
 #endif
 }
 
+
+// The frame's drain, fused.  Once nothing is left to claim and few paths are alive, an iteration
+// of separate launches costs about as long as its slowest ray whatever the number of paths (one
+// extend launch lasts ~300 us for a query of ~300 steps), and a path of the last claims may need
+// max_bounce_count more iterations.  So when k_bookkeep sets Counters::fused (see ResPlan::fuse),
+// the next iteration launched with these kernels runs every remaining path to its end in one
+// launch: k_drain_list gathers the live slots, then each k_drain lane takes a path and loops
+// extend -> shade_bounce -> connect -> prologue of the next bounce until the path ends, then
+// splats it.  Lanes take new paths as theirs end (at bounce boundaries: a wave syncs on its
+// slowest traversal per bounce, not the whole launch per bounce).  The functions are the ones the
+// separate kernels run (ray_prologue, Traversal, shade_bounce, splat_sample), so a path's
+// result is the same bits; the order in which paths finish does not enter any result.
+//
+// k_drain_list (the fused iteration, after k_generate splatted the last finished array): the
+// survivors of the last k_shade (S_TRACE) go to Pool::sh_slot, sharded like the queues; the
+// finished arrays are emptied (their entries are splatted already).
+__global__ void __launch_bounds__(BLOCK) k_drain_list(Pool pool, Counters* cnt) {
+    if (!cnt->fused || cnt->done) return;                              // uniform
+    const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
+    const bool live = slot < pool.n && pool.state[slot] == S_TRACE;
+    if (slot < pool.n && (slot & 63u) == 0) pool.fin_w[slot >> 6] = 0;
+    const uint32_t shard = blockIdx.x % NSHARD;
+    __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
+    const bool tp[1] = {live};
+    uint32_t* const tc[1] = {&cnt->drain_count[shard][0]};
+    uint32_t tpos[1], ttot[1];
+    block_tally<BLOCK, 1>(tp, tc, tpos, ttot, tally);
+    if (live) pool.sh_slot[(size_t)shard*pool.shard_cap + tpos[0]] = slot;
+}
+
+// k_drain — the rest of every live path (see above).  Persistent waves fetch CHUNK slots of
+// the list per atomic, like k_trace.  Ray counts as the separate kernels make them: a closest
+// ray per continuation, a shadow ray per NEE cast, "traced" for the rays that enter a BVH.
+template <bool LST, bool ENV>
+__global__ void __launch_bounds__(TB) k_drain(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
+                                              uint2* spill) {
+    if (!cnt->fused || cnt->done) return;                              // uniform
+    __shared__ uint2 lds_stack[STACK_LDS*TB];
+    Stack stk;
+    stk.lds = lds_stack; stk.spill = spill; stk.lane = threadIdx.x; stk.block = TB;
+    stk.gtid = blockIdx.x*TB + threadIdx.x; stk.nthreads = gridDim.x*TB;
+    __shared__ uint32_t qlen[NSHARD];
+    if (threadIdx.x < NSHARD) qlen[threadIdx.x] = cnt->drain_count[threadIdx.x][0];
+    __syncthreads();
+    uint32_t shard = blockIdx.x % NSHARD, tried = 0;
+    const uint32_t lane = __lane_id();
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    uint32_t chunk_next = 0, chunk_end = 0;
+    bool exhausted = false, active = false, fresh = false;
+    uint32_t n_closest = 0, n_shadow = 0, n_traced = 0, n_traced_sh = 0;
+    // the lane's path
+    uint32_t slot = 0;
+    V3 ro = {0, 0, 0}, rd = {0, 0, 0}, thr = {0, 0, 0}, total = {0, 0, 0};
+    float prev_pdf = 0.0f, vig = 0.0f;
+    uint32_t bounce = 0, is_spec = 0, pixel = 0, key = 0, p = 0;
+    int32_t at = 0;
+    Rng rng = {0, 0, 0, 0};
+    Prologue pro = {};
+    for (;;) {
+        // idle lanes take the next live slots
+        unsigned long long idle = __ballot(!active);
+        while (idle && !exhausted) {
+            if (chunk_next >= chunk_end) {
+                const int leader = __ffsll((long long)__ballot(true)) - 1;
+                bool got = false;
+                while (tried < NSHARD) {
+                    uint32_t* head = &cnt->drain_fetch[shard][0];
+                    const uint32_t len = qlen[shard];
+                    uint32_t base = 0xFFFFFFFFu;
+                    if (lane == (uint32_t)leader &&
+                        __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < len)
+                        base = atomicAdd(head, CHUNK);
+                    base = __shfl(base, leader);
+                    if (base < len) {
+                        chunk_next = shard*pool.shard_cap + base;
+                        chunk_end = shard*pool.shard_cap + min(base + CHUNK, len);
+                        got = true;
+                        break;
+                    }
+                    shard = (shard + 1) % NSHARD;
+                    ++tried;
+                }
+                if (!got) { exhausted = true; break; }
+            }
+            const uint32_t avail = chunk_end - chunk_next;
+            const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+            if (!active && rank < avail) {
+                slot = pool.sh_slot[chunk_next + rank];
+                const float4 o4 = ldnt(&pool.ray_o[slot]), d4 = ldnt(&pool.ray_d[slot]);
+                const float4 t4 = ldnt(&pool.thr[slot]), L4 = ldnt(&pool.L[slot]);
+                const float2 pn2 = ldnt(&pool.prev_n[slot]);
+                const uint4 r4 = ldnt(&pool.rng[slot]);
+                ro = ld3(o4); rd = ld3(d4); thr = ld3(t4); total = ld3(L4); vig = t4.w;
+                prev_pdf = pn2.x; p = __float_as_uint(pn2.y);
+                const uint32_t flags = __float_as_uint(L4.w);
+                bounce = flags & 0xFFu; is_spec = (flags >> 8) & 1u; at = (int32_t)((flags >> 9) & 0x7Fu);
+                pixel = __float_as_uint(o4.w); key = __float_as_uint(d4.w);
+                rng = {r4.x, r4.y, r4.z, r4.w};
+                active = true;
+                fresh = true;
+            }
+            chunk_next += min((uint32_t)__popcll(idle), avail);
+            idle = __ballot(!active);
+        }
+        if (__ballot(active) == 0ull) break;
+        // the closest hit: the ray prologue (the same result k_shade / k_generate stored with the
+        // path), then the BVH walk for a ray that meets a mesh
+        if (active) pro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
+        // a fresh path's ray is counted already (k_bookkeep: alive / cast, and its queue entry)
+        n_traced += (active && !fresh && pro.bvh) ? 1u : 0u;
+        fresh = false;
+        Hit h;
+        h.t = pro.t; h.code = pro.code; h.tri = 0; h.v = 0.0f; h.w = 0.0f;
+        {
+            Traversal<false, LST> tr;
+            bool tracing = active && pro.bvh;
+            if (tracing) {
+                tr.init_rec(sc, stk, ro, rd, pro.inv_d, pro.t, 0u, pro.mlist);
+                tracing = tr.mode != TM_DONE;
+            }
+            while (__ballot(tracing)) {
+                if (tracing && !tr.step(sc, stk)) tracing = false;
+            }
+            if (active && pro.bvh && tr.code != RT_HIT_MISS) h = tr.result();
+        }
+        // one bounce
+        bool done = false, cast_shadow = false;
+        V3 sh_o = {0, 0, 0}, sh_d = {0, 0, 0}, sh_c = {0, 0, 0};
+        float sh_t = 0.0f;
+        uint32_t sh_light = 0;
+        if (active) {
+            const uint32_t canonical = fp.frame_count + (fp.list_xy ? fp.list_s[key] : key);
+            const SamplerState ss = {pixel % fp.w, pixel / fp.w, canonical, st.sampling_strategy};
+#if RT_SHADE_PROF
+            unsigned long long prof[SP_N] = {};
+#endif
+            done = shade_bounce<ENV>(sc, st, ss, pool, slot, h, ro, rd, thr, total, prev_pdf, bounce, is_spec, at, rng,
+                                     cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light SP_PASS);
+        }
+        // intersect_shadow_ray (:756): the prologue, then the BVH walk; the NEE term is added last
+        // in the bounce, as k_connect adds it (:768)
+        {
+            Prologue spro = {};
+            if (cast_shadow) spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
+            Traversal<true, LST> tr;
+            bool tracing = cast_shadow && !spro.occluded && spro.bvh;
+            n_traced_sh += tracing ? 1u : 0u;
+            if (tracing) {
+                tr.init_rec(sc, stk, sh_o, sh_d, spro.inv_d, sh_t, sh_light, spro.mlist);
+                tracing = tr.mode != TM_DONE;
+            }
+            while (__ballot(tracing)) {
+                if (tracing && !tr.step(sc, stk)) tracing = false;
+            }
+            if (cast_shadow && !spro.occluded && (!spro.bvh || !tr.occluded)) total = add(total, sh_c);
+        }
+        n_shadow += cast_shadow ? 1u : 0u;
+        if (active && done) {
+            const uint32_t s = fp.list_xy ? fp.list_s[key] : key;
+            const V2 j = sample_jitter(sc, st, fp, pixel % fp.w, pixel / fp.w, s);
+            splat_sample(fp, pool, total, vig, make_float2(j.x, j.y), key, p);
+            active = false;
+        } else if (active) {
+            ++n_closest;                                  // the next bounce's intersect_scene
+        }
+    }
+    // the pool's material stacks were written at the path's slot (shade_bounce); nothing else of
+    // the pool is read again.  Counts: one atomic per wave each.
+    unsigned long long c[4] = {n_closest, n_shadow, n_traced, n_traced_sh};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        for (int m = 32; m; m >>= 1) c[k] += __shfl_xor(c[k], m);
+    if (lane == 0) {
+        if (c[0]) atomicAdd(&cnt->closest_rays, c[0]);
+        if (c[1]) atomicAdd(&cnt->shadow_rays, c[1]);
+        if (c[2]) atomicAdd(&cnt->traced_rays[0], c[2]);
+        if (c[3]) atomicAdd(&cnt->traced_rays[1], c[3]);
+    }
+}
 
 // k_resolve — splat_filter as a gather (RT/raytracer.cpp:187-259, :476-488).
 // Every output pixel sums its neighbours' samples in exactly the order the
@@ -2458,7 +2668,9 @@ __global__ void __launch_bounds__(256) k_combine_partials(float4* accum, const f
 // once there are plan.chunk of them (or all that remain, BK_FINAL), and the claim
 // limit moves to keep the ring from overwriting passes not yet resolved.
 enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
-struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life; };
+// fuse: set Counters::fused once nothing is left to claim and at most this many paths are alive
+// (0: never; see k_drain)
+struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse; };
 #ifndef RT_BK_THREADS
 #define RT_BK_THREADS 1024
 #endif
@@ -2476,73 +2688,104 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         }
         return;
     }
-    __shared__ uint32_t skip;
-    if (t == 0) {
-        skip = phase == BK_ITER && cnt->done;           // the partition finished in an earlier iteration
-        if (skip) cnt->res_from = cnt->res_to = 0;      // its last passes are resolved already
-        if (phase == BK_ITER && !skip) {
-            const unsigned long long rem = remaining_samples(cnt);
-            cnt->next_sample += ((unsigned long long)cnt->gen_free < rem ? (unsigned long long)cnt->gen_free : rem);
-            uint32_t ext = 0, sh = 0, pend = 0, tq = 0, ts = 0, ps = 0;
-            for (int k = 0; k < NSHARD; ++k) {
-                ext += cnt->cast[0][k][0] + cnt->alive[k][0];
-                sh += cnt->cast[1][k][0];
-                pend += cnt->alive[k][0];
-                ps += cnt->unsplat[k][0];
-                cnt->unsplat[k][0] = 0;
-                tq += cnt->ext_count[cur][k][0];
-                ts += cnt->shadow_count[k][0];
-                cnt->cast[0][k][0] = 0;
-                cnt->cast[1][k][0] = 0;
-                cnt->alive[k][0] = 0;
-                cnt->ext_count[cur][k][0] = 0;
-                cnt->shadow_count[k][0] = 0;
-                cnt->fetch[0][k][0] = 0;
-                cnt->fetch[1][k][0] = 0;
-            }
-            cnt->closest_rays += ext;
-            cnt->shadow_rays += sh;
-            cnt->traced_rays[0] += tq;
-            cnt->traced_rays[1] += ts;
-            cnt->pending = pend;
-            cnt->pending_splat = ps;
-            // nothing left to claim, trace or splat: every record is in the ring
-            const bool complete = cnt->next_sample >= cnt->total_samples && pend == 0 && ps == 0;
-            if (complete) cnt->done = 1;
-            const uint32_t it = cnt->iter++;
-            cnt->hist[it & 127u] = cnt->next_sample;
-            if (plan.mode) {
-                const unsigned long long done = it >= plan.life ? cnt->hist[(it - plan.life) & 127u] : cnt->start_sample;
-                const uint32_t done_pass = complete ? plan.pass1 : (uint32_t)(done / plan.P);
-                const uint32_t from = cnt->res_cursor;
-                cnt->res_from = cnt->res_to = 0;
-                if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
-                    cnt->res_from = from;
-                    cnt->res_to = done_pass;
-                    cnt->res_cursor = done_pass;
-                    // the ring slots of [from, done_pass) are free once the resolve launched next has run
-                    cnt->claim_limit = (unsigned long long)(done_pass + plan.ring)*plan.P;
-                }
-            }
-        }
-        carry = 0;
-    }
-    __syncthreads();
-    if (skip) return;
-    // exclusive scan of free_n: thread t owns the contiguous entries [t*E, t*E + E), sums them
-    // (all loads in flight), then a wave scan by shuffles and one barrier for the 16 wave totals.
-    // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
-    // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
+    // The free counts' loads go out first, so they overlap the counter work below.
     // Up to BK_EMAX entries per thread (pools up to 32k blocks, 8.4M paths) are loaded at once into
     // registers, all in flight, and the claims are written from them; a loop covers larger pools.
     constexpr uint32_t BK_EMAX = 32*(1024 / BK_THREADS);
     const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
     const uint32_t lo = t*E, hi = min(lo + E, nblocks);
-    uint32_t sum = 0;
     uint32_t v[BK_EMAX];
     if (E <= BK_EMAX) {
 #pragma unroll
         for (uint32_t j = 0; j < BK_EMAX; ++j) v[j] = lo + j < hi ? pool.free_n[lo + j] : 0u;
+    }
+    __shared__ uint32_t skip;
+    if (t < 64) {
+        // Lane k < NSHARD reads shard k's counters, all loads in flight, and the sums come from
+        // shuffles.  (Thread 0 alone walking the shards, each load ordered behind the previous
+        // shard's stores, took ~60 dependent round trips: 27 us alone, ~290 us beside the other
+        // partitions' kernels, 10 % of a partition's iteration.)
+        const bool it_phase = phase == BK_ITER;
+        const uint32_t done_flag = it_phase ? cnt->done : 0u;
+        uint32_t c0 = 0, al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
+        if (it_phase && t < NSHARD) {
+            c0 = cnt->cast[0][t][0];
+            al = cnt->alive[t][0];
+            c1 = cnt->cast[1][t][0];
+            us = cnt->unsplat[t][0];
+            eq = cnt->ext_count[cur][t][0];
+            sq = cnt->shadow_count[t][0];
+        }
+        unsigned long long next = 0, total = 0, lim = 0, start = 0;
+        uint32_t gfree = 0, it = 0, rcur = 0;
+        if (t == 0 && it_phase) {
+            next = cnt->next_sample; total = cnt->total_samples; lim = cnt->claim_limit;
+            start = cnt->start_sample; gfree = cnt->gen_free; it = cnt->iter; rcur = cnt->res_cursor;
+        }
+        // the claim cursor `life` iterations ago (loaded before any store to the counters)
+        const unsigned long long done_cursor =
+            (t == 0 && it_phase && plan.mode && it >= plan.life) ? cnt->hist[(it - plan.life) & 127u] : start;
+        const bool sk = it_phase && done_flag;
+        if (it_phase && !sk && t < NSHARD) {
+            cnt->unsplat[t][0] = 0;
+            cnt->cast[0][t][0] = 0;
+            cnt->cast[1][t][0] = 0;
+            cnt->alive[t][0] = 0;
+            cnt->ext_count[cur][t][0] = 0;
+            cnt->shadow_count[t][0] = 0;
+            cnt->fetch[0][t][0] = 0;
+            cnt->fetch[1][t][0] = 0;
+        }
+        uint32_t ext = c0 + al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
+#pragma unroll
+        for (int off = 1; off < NSHARD; off <<= 1) {
+            ext += __shfl_xor(ext, off); sh += __shfl_xor(sh, off); pend += __shfl_xor(pend, off);
+            ps += __shfl_xor(ps, off); tq += __shfl_xor(tq, off); ts += __shfl_xor(ts, off);
+        }
+        if (t == 0) {
+            skip = sk;
+            if (sk) cnt->res_from = cnt->res_to = 0;        // its last passes are resolved already
+            if (it_phase && !sk) {
+                const unsigned long long lm = lim < total ? lim : total;
+                const unsigned long long rem = lm > next ? lm - next : 0ull;      // remaining_samples()
+                next += ((unsigned long long)gfree < rem ? (unsigned long long)gfree : rem);
+                cnt->next_sample = next;
+                cnt->closest_rays += ext;
+                cnt->shadow_rays += sh;
+                cnt->traced_rays[0] += tq;
+                cnt->traced_rays[1] += ts;
+                cnt->pending = pend;
+                cnt->pending_splat = ps;
+                // nothing left to claim, trace or splat: every record is in the ring
+                const bool complete = next >= total && pend == 0 && ps == 0;
+                if (complete) cnt->done = 1;
+                else if (plan.fuse && next >= total && pend <= plan.fuse) cnt->fused = 1;
+                cnt->iter = it + 1;
+                cnt->hist[it & 127u] = next;
+                if (plan.mode) {
+                    const uint32_t done_pass = complete ? plan.pass1 : (uint32_t)(done_cursor / plan.P);
+                    const uint32_t from = rcur;
+                    cnt->res_from = cnt->res_to = 0;
+                    if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
+                        cnt->res_from = from;
+                        cnt->res_to = done_pass;
+                        cnt->res_cursor = done_pass;
+                        // the ring slots of [from, done_pass) are free once the resolve launched next has run
+                        cnt->claim_limit = (unsigned long long)(done_pass + plan.ring)*plan.P;
+                    }
+                }
+            }
+            carry = 0;
+        }
+    }
+    __syncthreads();
+    if (skip) return;
+    // exclusive scan of free_n: thread t owns the contiguous entries [t*E, t*E + E), sums them,
+    // then a wave scan by shuffles and one barrier for the 16 wave totals.
+    // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
+    // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
+    uint32_t sum = 0;
+    if (E <= BK_EMAX) {
 #pragma unroll
         for (uint32_t j = 0; j < BK_EMAX; ++j) sum += v[j];
     } else {
@@ -2716,6 +2959,7 @@ struct rt_scene {
     size_t tile_base_cap = 0;
     uint32_t trace_grid = 0;        // persistent k_trace blocks (extend)
     uint32_t connect_grid = 0;      // persistent k_trace<true> blocks (<= trace_grid: the spill area)
+    uint32_t drain_grid = 0;        // persistent k_drain blocks (<= trace_grid: the spill area)
     float4* d_samp = nullptr;       // per-sample records for the deterministic splat
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
@@ -3067,13 +3311,18 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(s->start_ev, stream));
-    struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live, drain; int final_buf;
+    struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live, drain, near;
+                 unsigned long long seen_next; int final_buf;
                  uint64_t chunk_first[2]; int chunk_n[2]; uint32_t pass0, pass1, ring; float4* dst;
                  bool res_ev[EV_SLOTS]; };
     Run run[MAX_PARTITIONS] = {};
     double kms[RT_KERNEL_COUNT] = {};
     uint64_t klaunch[RT_KERNEL_COUNT] = {};
     const uint32_t life = std::max<uint32_t>(st->max_bounce_count, 1u);
+    // live paths at which the drain is fused (k_drain): as many as its grid has lanes; RT_FUSE_PATHS
+    // another count (0 = never), read per frame
+    const char* fz = getenv("RT_FUSE_PATHS");
+    const uint32_t fuse_paths = fz ? (uint32_t)strtoul(fz, nullptr, 10) : s->drain_grid*TB;
     for (int k = 0; k < nparts; ++k) {
         int err = ensure_partition(s, k);
         if (!err) err = ensure_pool(s->part[k], pool_n);
@@ -3114,6 +3363,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             }
         }
         init.start_sample = init.next_sample;
+        r.seen_next = init.next_sample;
         pt.cnt_host[2] = init;           // pinned: the copy is asynchronous (the frame ends before the next write)
         HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + 2, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
@@ -3129,7 +3379,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     }
     auto plan_of = [&](int k, uint32_t mode) {
         const Run& r = run[k];
-        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, life};
+        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, life, fuse_paths};
     };
     // Stage timing without extra host syncs: each iteration records begin/end
     // events into one of EV_SLOTS ring slots; a chunk's slots are read back when
@@ -3163,23 +3413,37 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         auto e = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
         const Pool pv = pool_view(pt.pool, r.cur);        // the path buffers swap every iteration
         const int sparse = r.drain ? 1 : 0;
+        // near the drain every iteration carries the fused-drain kernels; they run only in the
+        // iteration after k_bookkeep set Counters::fused, whose extend / shade / connect then exit
+        const int fuse = (r.near && fuse_paths) ? 1 : 0;
         b(RT_KERNEL_GENERATE);
         k_generate<<<r.grid, BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
-        e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
-        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
-        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
+        e(RT_KERNEL_GENERATE);
+        if (fuse) {
+            k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
+            if (s->ds.listed_only) {
+                if (env) k_drain<true, true><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<true, false><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+            } else {
+                if (env) k_drain<false, true><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<false, false><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+            }
+        }
+        b(RT_KERNEL_EXTEND);
+        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         if (env) {
-            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
-            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
+            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
+            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         } else if (s->ds.blob_q) {
-            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
+            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         } else {
-            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse);
+            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
-        else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag);
+        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
         e(RT_KERNEL_CONNECT);
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
@@ -3245,6 +3509,10 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             ++r.consumed;
             const Counters& c = s->part[k].cnt_host[b];
             if (c.next_sample >= c.total_samples) r.drain = true;     // the chunks enqueued from now on
+            // the claims of a few more chunks reach the end: from now on the iterations carry the
+            // fused-drain kernels (two chunks are in flight when the host sees a chunk's counters)
+            if (c.next_sample + 2*(c.next_sample - r.seen_next) >= c.total_samples) r.near = true;
+            r.seen_next = c.next_sample;
             if (c.next_sample >= c.total_samples && c.pending == 0 && c.pending_splat == 0) {
                 r.live = false; r.final_buf = b; --live;       // its chunk still in flight finds nothing to do
                 int err = finish(k);
@@ -3714,6 +3982,10 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         if (const char* e = getenv("RT_CONNECT_GRID_PCT")) connect_pct = std::max(1, atoi(e));
         s->connect_grid = std::min(s->trace_grid,
                                    std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)connect_pct / 100ull)));
+        int drain_cu = 0;     // k_drain holds ~220 VGPRs: 2 waves per SIMD; its grid is what fits at once
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&drain_cu, k_drain<false, false>, TB, 0) != hipSuccess || drain_cu < 1)
+            drain_cu = 1;
+        s->drain_grid = std::min(s->trace_grid, (uint32_t)(prop.multiProcessorCount*drain_cu));
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }

@@ -374,3 +374,41 @@ def test_rcp_cr_exhaustive(rt):
     assert rt.lib().rt_debug_verify_rcp(0, C.byref(bad), C.byref(first)) == 0
     REPORT["rcp_cr_exhaustive"] = {"inputs": 1 << 32, "mismatches": bad.value}
     assert bad.value == 0, f"first mismatch at bits 0x{first.value:08x}"
+
+
+@pytest.mark.parametrize("which,w,h,spp", [("c3small", 192, 108, 24), ("c4small", 192, 108, 16), ("c1", 256, 256, 16)])
+def test_fused_drain_matches_separate_kernels(which, w, h, spp, request, monkeypatch):
+    """The frame's drain fused into k_drain (each lane runs a path's remaining bounces) computes
+    the same per-sample bits as the separate extend / shade / connect launches: frames (exact and
+    streaming splat), per-sample radiance of the explicit-sample path and every ray count are
+    identical whether the drain is never fused (RT_FUSE_PATHS=0), fused at the default count
+    or fused with every path still alive (a count above the pool)."""
+    rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
+    st = type(st).from_buffer_copy(st)
+    st.samples_per_pixel = spp
+    rng = np.random.default_rng(11)
+    xy = rng.integers(0, [w, h], size=(20000, 2)).astype(np.uint32)
+    s = rng.integers(0, spp, size=20000).astype(np.uint32)
+    out = {}
+    for name, val in (("off", "0"), ("default", None), ("all", "1000000000")):
+        if val is None:
+            monkeypatch.delenv("RT_FUSE_PATHS", raising=False)
+        else:
+            monkeypatch.setenv("RT_FUSE_PATHS", val)
+        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+            ex, es = dev.render(cam, st, fc, w, h)
+        sm, ss = dev.render(cam, st, fc, w, h)
+        samp, ts = dev.trace_samples(cam, st, w, h, xy, s)
+        out[name] = (ex, sm, samp, [(int(x.closest_hit_rays), int(x.shadow_rays), int(x.traced_rays[0]),
+                                     int(x.traced_rays[1])) for x in (es, ss, ts)], int(ss.iterations))
+    ref = out["off"]
+    REPORT[f"fused_drain_{which}"] = {k: {"frames_equal": bool(np.array_equal(v[0], ref[0]) and np.array_equal(v[1], ref[1])),
+                                          "samples_equal": bool(np.array_equal(v[2], ref[2])), "rays": v[3],
+                                          "iterations": v[4]} for k, v in out.items()}
+    for name in ("default", "all"):
+        ex, sm, samp, rays, _ = out[name]
+        assert rays == ref[3], name
+        assert np.array_equal(ex, ref[0]), name
+        assert np.array_equal(sm, ref[1]), name
+        assert np.array_equal(samp, ref[2]), name
+    assert out["all"][4] < out["off"][4]          # the fused drain ended the frame in fewer iterations

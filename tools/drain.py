@@ -13,7 +13,8 @@ import argparse
 import csv
 
 SHORT = {"k_generate": "gen", "k_trace<false>": "ext", "k_shade": "shd", "k_trace<true>": "con",
-         "k_bookkeep": "bk", "k_resolve_tiles": "res", "k_combine_partials": "comb", "k_pixel_map": "map"}
+         "k_bookkeep": "bk", "k_resolve_tiles": "res", "k_combine_partials": "comb", "k_pixel_map": "map",
+         "k_drain_list": "dl", "k_drain": "drn"}
 
 
 def kname(n):
@@ -52,7 +53,7 @@ def main():
         last = max(e for it in its for _, s, e in it)
         print(f"\npartition {key}={pid}: {len(its)} iterations, kernel time {busy / 1e6:.2f} ms, "
               f"ends at {last / 1e6:.2f} ms")
-        print("  it  start_ms  len_ms  gap_ms | " + " ".join(f"{k:>6s}" for k in ("gen", "ext", "shd", "con", "bk", "res")))
+        print("  it  start_ms  len_ms  gap_ms | " + " ".join(f"{k:>6s}" for k in ("gen", "dl", "drn", "ext", "shd", "con", "bk", "res")))
         for i, it in enumerate(its):
             s = it[0][1]
             e = max(x[2] for x in it)
@@ -60,7 +61,7 @@ def main():
             d = {}
             for n, ss, ee in it:
                 d[n] = d.get(n, 0) + (ee - ss)
-            cols = " ".join(f"{d[k] / 1e3:6.0f}" if k in d else "     -" for k in ("gen", "ext", "shd", "con", "bk", "res"))
+            cols = " ".join(f"{d[k] / 1e3:6.0f}" if k in d else "     -" for k in ("gen", "dl", "drn", "ext", "shd", "con", "bk", "res"))
             print(f"  {i:3d} {s / 1e6:8.2f} {(e - s) / 1e6:7.3f} {gap / 1e6:7.3f} | {cols}")
 
 
