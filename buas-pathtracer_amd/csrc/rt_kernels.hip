@@ -3239,11 +3239,13 @@ inline bool debug_timing() { static const bool on = getenv("RT_DEBUG_TIMING") !=
 // shard's pixels; 0 = an explicit sample list).  A larger pool amortizes each trace
 // launch's tail (its slowest ray) over more rays, until the pool is so large that the
 // frame is only a few pool fills and the final drain dominates: a fifth of the
-// partition's samples, between 2^21 and 3 x 2^21 (~5 GB of path state and queues).  r01,
+// partition's samples, between 2^21 and 4 x 2^21 (~6.5 GB of path state and queues).  r01,
 // C3 256 spp on one box: 1M 6552, 2M 8128, 4M 8613 / 8895, 6M 9058, 8M 9054 Mrays/s.
 // With the compacted pool (r02) a larger pool costs less: rank 0 of 8 (16.6M samples per
 // partition) 1M 53.9, 2M 44.6, 3M 42.7, 4M 43.1 ms; an eighth (2M) became a fifth (3.3M):
-// 45.0 -> 43.4 ms (2 pairs), the full frame and rank 0 of 4 unchanged.
+// 45.0 -> 43.4 ms (2 pairs), the full frame and rank 0 of 4 unchanged.  With the fused drain the
+// full frame gains from 8M paths (6.3M 239.3 / 239.4, 8.4M 236.7 / 237.6, 10.5M 237.7 / 238.8, 12.6M
+// 239.8 / 240.3 ms): the upper bound is 4 x 2^21 (rank 0 of 2 at 8.4M: 128.7 -> 128.8 / 129.2, unchanged).
 struct FrameShape { int nparts; uint32_t pool_n; };
 #ifndef RT_POOL_DIV
 #define RT_POOL_DIV 5ull
@@ -3256,7 +3258,7 @@ FrameShape frame_shape(unsigned long long total, uint32_t passes) {
     uint32_t pool_n = g_pool_override;
     if (!pool_n) {
         const unsigned long long want = total / (unsigned long long)f.nparts / RT_POOL_DIV;
-        pool_n = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>(want, 1ull << 21), 3ull << 21);
+        pool_n = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>(want, 1ull << 21), 4ull << 21);
     }
     // small frames: one partition, pool no larger than the work
     if ((unsigned long long)pool_n*f.nparts > total) f.nparts = 1;
