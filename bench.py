@@ -253,7 +253,10 @@ def main():
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             ent = tj.get("kernels", {}).get(KERNEL[dom]) if tj.get("config") == args.config else None
-            if ent:
+            # measured on launches of the same size (units per launch within 10 %), else stale
+            same = ent and (not ent.get("units_per_launch") or
+                            abs(ent["units_per_launch"] / max(units_per_launch, 1.0) - 1.0) <= 0.1)
+            if ent and same:
                 traffic = ent["hbm_bytes_per_launch"]
                 iso_gbs = alg_bytes / (ent["isolated_mean_us"] * 1e-6) / 1e9
                 isolated = {"mean_launch_ms": round(ent["isolated_mean_us"] / 1e3, 4), "achieved": round(iso_gbs, 1),

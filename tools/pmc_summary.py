@@ -16,7 +16,7 @@ import json
 import os
 
 KERNELS = ["k_generate", "k_trace<false", "k_shade", "k_trace<true", "k_splat", "k_resolve_tiles", "k_resolve",
-           "k_combine_partials", "k_bookkeep"]
+           "k_combine_partials", "k_bookkeep", "k_drain_list", "k_drain"]
 LABEL = {"k_trace<false": "k_extend (k_trace<false, .>)", "k_trace<true": "k_connect (k_trace<true, .>)"}
 KEYS = {"k_trace<false": "k_extend", "k_trace<true": "k_connect"}
 
@@ -117,7 +117,13 @@ def main():
         if a.bench_log and os.path.exists(a.bench_log):
             for line in open(a.bench_log):
                 if line.startswith("{"):
-                    rec["bench_spp"] = json.loads(line)["config"].get("spp")
+                    b = json.loads(line)
+                    rec["bench_spp"] = b["config"].get("spp")
+                    # the units per launch of the dominant kernel in that run: bench.py uses the isolated
+                    # time only for launches of the same size
+                    rf = b.get("roofline") or {}
+                    if rf.get("kernel") in rec["kernels"]:
+                        rec["kernels"][rf["kernel"]]["units_per_launch"] = rf.get("units_per_launch")
         json.dump(rec, open(a.traffic, "w"), indent=1)
         print("wrote", a.traffic)
 
