@@ -3946,8 +3946,15 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         put(BLOB_INV, inv.data(), inv.size()*sizeof(M34));
         put(BLOB_FWD, fwd.data(), fwd.size()*sizeof(M34));
         put(BLOB_LIGHTS, d->lights, (size_t)d->light_count*sizeof(uint32_t));
+#if RT_PROLOGUE_SCALAR
+        // the prologue reads the top-level sequences and leaf records from HBM through the scalar
+        // cache (scene_in_lds does not rebase them): not copied into LDS (C3: 5 KB -> ~2 KB per block)
+        put(BLOB_TOP_SEQ, nullptr, 0);
+        put(BLOB_LEAF_REC, nullptr, 0);
+#else
         put(BLOB_TOP_SEQ, top_seq_host.data(), top_seq_host.size()*sizeof(float4));
         put(BLOB_LEAF_REC, leaf_rec_host.data(), (size_t)d->bvh_index_count*LEAF_REC_Q*sizeof(float4));
+#endif
         put(BLOB_MESHES, meshes.data(), meshes.size()*sizeof(DevMesh));
 #if RT_LDS_STRATA
         put(BLOB_STRATA, rt_dev_strata_tab, sizeof(rt_dev_strata_tab));
