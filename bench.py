@@ -126,6 +126,10 @@ def main():
     ap.add_argument("--height", type=int, default=0)
     ap.add_argument("--pool", type=int, default=0, help="in-flight path pool size (0 = default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shard-index", type=int, default=0, help="with --shard-of: which rank's share (diagnostic)")
+    ap.add_argument("--shard-mode", choices=["tiles", "passes"], default="passes",
+                    help="what a rank's share of the frame is: a range of sample passes over every tile (default: "
+                         "equal cost per rank whatever the content) or tiles t %% N (DESIGN.md section 7)")
     ap.add_argument("--shard-of", type=int, default=0,
                     help="diagnostic (1 process): render only rank 0's tiles of an N-rank frame, to size the "
                          "per-rank work of the N-GPU strong-scaling run; not a bench line")
@@ -166,6 +170,7 @@ def main():
         rt.lib().rt_set_path_pool(args.pool)
     if args.env_sampling:
         rt.set_env_sampling(args.env_sampling)
+    rt.set_shard_mode(rt.abi.RT_SHARD_PASSES if args.shard_mode == "passes" else rt.abi.RT_SHARD_TILES)
     dev = rt.DeviceScene(scene, device)
     accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{device}")
     stream = torch.cuda.current_stream(device)
@@ -180,8 +185,8 @@ def main():
 
     def step():
         accum.zero_()
-        if args.shard_of > 1:                          # diagnostic: rank 0's share of an N-rank frame
-            return render_shard(0, args.shard_of, accum)
+        if args.shard_of > 1:                          # diagnostic: one rank's share of an N-rank frame
+            return render_shard(args.shard_index, args.shard_of, accum)
         # tiles t % world == rank into a zeroed frame buffer, the RCCL sum-reduce of it over
         # xGMI into rank 0, which adds it to its accumulation buffer
         return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch)
@@ -331,7 +336,7 @@ def main():
                                    f"depth {st.max_bounce_count}" + (" env-sampling" if args.env_sampling else ""),
                        "width": w, "height": h,
                        "spp": st.samples_per_pixel, "max_depth": st.max_bounce_count,
-                       "parallelism": (f"tiles%{args.shard_of} (rank 0 only, diagnostic)" if args.shard_of > 1 else f"tiles%{world}" + ("+rccl_reduce" if world > 1 else ""))},
+                       "parallelism": (f"{args.shard_mode}%{args.shard_of} (rank {args.shard_index} only, diagnostic)" if args.shard_of > 1 else f"{args.shard_mode}%{world}" + ("+rccl_reduce" if world > 1 else ""))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": KERNEL[dom], "bytes_per_unit": BYTES_PER_UNIT[dom],

@@ -314,6 +314,12 @@ def set_splat_mode(mode):
     _check(lib().rt_set_splat_mode(int(mode)))
 
 
+def set_shard_mode(mode):
+    """rt_set_shard_mode: abi.RT_SHARD_TILES (default: tile t to shard t % n) or RT_SHARD_PASSES
+    (every tile, a contiguous range of the sample passes per shard)."""
+    _check(lib().rt_set_shard_mode(int(mode)))
+
+
 class splat_mode:
     """with splat_mode(abi.RT_SPLAT_EXACT): ... restores the default (streaming) splat after."""
 

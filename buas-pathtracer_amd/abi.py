@@ -25,6 +25,7 @@ RT_MATERIAL_EMISSIVE = 0x4
 RT_PRIMITIVE_NONE, RT_PRIMITIVE_PLANE, RT_PRIMITIVE_SPHERE, RT_PRIMITIVE_BOX, RT_PRIMITIVE_MESH = range(5)
 RT_SAMPLING_UNIFORM, RT_SAMPLING_OPTIMIZED_BLUE_NOISE, RT_SAMPLING_STRATIFIED = range(3)
 RT_SPLAT_STREAM, RT_SPLAT_EXACT, RT_SPLAT_ATOMIC = range(3)          # rt_splat_mode
+RT_SHARD_TILES, RT_SHARD_PASSES = range(2)                           # rt_shard_mode
 RT_RNG_PER_SAMPLE, RT_RNG_TILE_STREAM = 0, 1
 RT_HIT_MISS = 0xFFFFFFFF
 RT_HIT_PLANE_BIT = 0x80000000
@@ -179,6 +180,7 @@ ABI_FUNCTIONS = {
     "rt_set_profiling_stages": (C.c_int, [C.c_uint32]),
     "rt_set_path_pool": (C.c_int, [C.c_uint32]),
     "rt_set_splat_mode": (C.c_int, [C.c_int]),
+    "rt_set_shard_mode": (C.c_int, [C.c_int]),
     "rt_set_env_sampling": (C.c_int, [C.c_int]),
     "rt_build_bvh": (C.c_int, [C.c_int, C.c_uint32, P(V3), P(V3), C.c_int, P(BvhNode), P(C.c_uint32), P(C.c_uint32)]),
     "rt_build_bvh_last_error": (C.c_char_p, []),

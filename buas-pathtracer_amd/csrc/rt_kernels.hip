@@ -41,6 +41,7 @@ uint32_t g_profiling = 0;       // stage mask: bit k = rt_kernel_stage k timed w
 uint32_t g_pool_override = 0;
 int g_splat_mode = RT_SPLAT_STREAM;
 int g_env_sampling = 0;         // rt_set_env_sampling
+int g_shard_mode = RT_SHARD_TILES;   // rt_set_shard_mode
 }
 
 // Tables embedded from data/ (extracted from the reference by tools/extract_tables.py).
@@ -3270,7 +3271,8 @@ FrameShape frame_shape(unsigned long long total, uint32_t passes) {
 // How a frame's samples reach the accumulation buffer (rt_set_splat_mode).
 struct SplatCfg {
     int mode = RT_SPLAT_ATOMIC;         // rt_splat_mode; ATOMIC also for explicit sample lists
-    uint32_t passes = 0;                // samples per pixel of the frame
+    uint32_t passes = 0;                // the frame's sample passes (of this shard)
+    uint32_t pass_lo = 0;               // its first pass (RT_SHARD_PASSES: the shard's range)
     uint32_t ring = 0, chunk = 0;       // STREAM: record-ring passes per partition, passes per resolve
     float4* rec = nullptr;              // STREAM: nparts rings of ring*P; EXACT: spp*P, pass-major
     float* rec_jy = nullptr;
@@ -3345,8 +3347,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             init.next_sample = total*(unsigned long long)k / nparts;
             init.total_samples = total*(unsigned long long)(k + 1) / nparts;
         } else {
-            r.pass0 = (uint32_t)((unsigned long long)sp.passes*k / nparts);
-            r.pass1 = (uint32_t)((unsigned long long)sp.passes*(k + 1) / nparts);
+            r.pass0 = sp.pass_lo + (uint32_t)((unsigned long long)sp.passes*k / nparts);
+            r.pass1 = sp.pass_lo + (uint32_t)((unsigned long long)sp.passes*(k + 1) / nparts);
             init.next_sample = (unsigned long long)r.pass0*fp.pixels;
             init.total_samples = (unsigned long long)r.pass1*fp.pixels;
             init.res_cursor = r.pass0;
@@ -3696,6 +3698,12 @@ int rt_set_path_pool(uint32_t paths) { g_pool_override = paths; return RT_OK; }
 int rt_set_env_sampling(int mode) {
     if (mode != 0 && mode != 1) { set_error("rt_set_env_sampling: mode must be 0 or 1"); return RT_ERROR_INVALID; }
     g_env_sampling = mode;
+    return RT_OK;
+}
+
+int rt_set_shard_mode(int mode) {
+    if (mode != RT_SHARD_TILES && mode != RT_SHARD_PASSES) { set_error("bad shard mode"); return RT_ERROR_INVALID; }
+    g_shard_mode = mode;
     return RT_OK;
 }
 
@@ -4087,15 +4095,18 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.tcx = (w + tiles->tile_w - 1) / tiles->tile_w;
     uint32_t tcy = (h + tiles->tile_h - 1) / tiles->tile_h;
     if (w > 65535 || h > 65535) { set_error("frame larger than 65535 pixels a side"); return RT_ERROR_INVALID; }
+    // RT_SHARD_PASSES: every tile, and the shard's range of sample passes (below)
+    const bool by_pass = g_shard_mode == RT_SHARD_PASSES && tiles->shard_count > 1;
+    const uint32_t tsi = by_pass ? 0u : tiles->shard_index, tsc = by_pass ? 1u : tiles->shard_count;
     auto& L = s->layout;
     const bool same = L.valid && L.w == w && L.h == h && L.tw == tiles->tile_w && L.th == tiles->tile_h &&
-                      L.si == tiles->shard_index && L.sc == tiles->shard_count;
+                      L.si == tsi && L.sc == tsc;
     if (!same) {
         // owned tiles: t % shard_count == shard_index, descending like the reference's queue (:555)
         L.valid = false;
         L.ids.clear(); L.prefix.assign(1, 0); L.owned_px = 0;
         for (uint32_t t = fp.tcx*tcy; t-- > 0;) {
-            if (t % tiles->shard_count != tiles->shard_index) continue;
+            if (t % tsc != tsi) continue;
             uint32_t min_x = tiles->tile_w*(t % fp.tcx), min_y = tiles->tile_h*(t / fp.tcx);
             uint32_t tw = std::min(w, min_x + tiles->tile_w) - min_x, th = std::min(h, min_y + tiles->tile_h) - min_y;
             L.ids.push_back(t);
@@ -4145,7 +4156,7 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     if (!same) {
         k_pixel_map<<<fp.ntiles, 256, 0, stream>>>(fp, s->d_pixmap);
         HIP_OK(hipGetLastError());
-        L.w = w; L.h = h; L.tw = tiles->tile_w; L.th = tiles->tile_h; L.si = tiles->shard_index; L.sc = tiles->shard_count;
+        L.w = w; L.h = h; L.tw = tiles->tile_w; L.th = tiles->tile_h; L.si = tsi; L.sc = tsc;
         L.blocks_ks = -1;
         L.valid = true;
     }
@@ -4155,7 +4166,11 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.kernel_size = (int32_t)filter->kernel_size;
     fp.cache_size = (int32_t)filter->cache_size;
     fp.accum = reinterpret_cast<float4*>(d_pixels);
-    unsigned long long total = (unsigned long long)fp.pixels*st->samples_per_pixel;
+    const uint32_t spp_all = st->samples_per_pixel;
+    const uint32_t pass_lo = by_pass ? (uint32_t)((unsigned long long)spp_all*tiles->shard_index / tiles->shard_count) : 0u;
+    const uint32_t pass_hi = by_pass ? (uint32_t)((unsigned long long)spp_all*(tiles->shard_index + 1) / tiles->shard_count)
+                                     : spp_all;
+    unsigned long long total = (unsigned long long)fp.pixels*(pass_hi - pass_lo);
     if (total == 0) { if (stats) memset(stats, 0, sizeof(*stats)); return RT_OK; }
     // The splat (rt_set_splat_mode).  Both deterministic modes keep a 20-byte record per
     // sample in HBM: STREAM a ring of `ring` passes per partition (k_resolve_tiles frees
@@ -4164,15 +4179,17 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     // less 16 GB for the partitions' path pools.  EXACT falls back to STREAM over budget or
     // past the filter radius k_resolve_tiles stages (12); STREAM to ATOMIC only if even
     // one pass per partition does not fit.
-    const uint32_t spp = st->samples_per_pixel;
+    const uint32_t spp = pass_hi - pass_lo;                       // this shard's passes
     const int ks = fp.cache_size ? fp.kernel_size : 0;
     const FrameShape shape = frame_shape(total, spp);
     int want_mode = g_splat_mode;
     if (const char* e = getenv("RT_SPLAT")) want_mode = atoi(e);
+    if (by_pass && want_mode == RT_SPLAT_EXACT) want_mode = RT_SPLAT_STREAM;   // k_resolve gathers passes 0..spp-1
     // the splat for a record budget (bytes): the mode, and for STREAM the ring and chunk
     auto plan_splat = [&](double budget, SplatCfg& sp, size_t& need_rec) {
         sp = SplatCfg{};
         sp.passes = spp;
+        sp.pass_lo = pass_lo;
         sp.mode = want_mode;
         need_rec = 0;
         if (sp.mode == RT_SPLAT_EXACT && (double)total*20.0 > budget) sp.mode = RT_SPLAT_STREAM;

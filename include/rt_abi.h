@@ -352,7 +352,7 @@ int rt_set_profiling(int enable);
 int rt_set_profiling_stages(uint32_t mask);
 
 /* Size of the in-flight path pool per partition (paths resident in HBM); 0 = default:
- * a fifth of the partition's samples, clamped to [2^21, 3 x 2^21]. */
+ * a fifth of the partition's samples, clamped to [2^21, 4 x 2^21]. */
 int rt_set_path_pool(uint32_t paths);
 
 /* How samples reach the accumulation buffer (splat_filter, RT/raytracer.cpp:187-259).
@@ -372,6 +372,20 @@ enum rt_splat_mode {
     RT_SPLAT_ATOMIC = 2,
 };
 int rt_set_splat_mode(int mode);
+
+/* What rt_tile_set::shard_index / shard_count split a frame by (multi-GPU: one shard per rank,
+ * the ranks' frames summed).  Either way every sample keeps its own key (frame, tile, pixel,
+ * sample), so the shards' frames sum to the single-GPU frame up to float summation order.
+ *   RT_SHARD_TILES (default): tile t belongs to shard t % shard_count (the reference's tile
+ *     queue, RT/raytracer.cpp:551-560, dealt out round robin).
+ *   RT_SHARD_PASSES: every tile, sample passes [spp*i/n, spp*(i+1)/n) of shard i of n: each
+ *     shard sees the whole image, so the shards' costs match whatever the content.  The
+ *     exact splat (RT_SPLAT_EXACT) is not split this way: such frames use RT_SPLAT_STREAM. */
+enum rt_shard_mode {
+    RT_SHARD_TILES  = 0,
+    RT_SHARD_PASSES = 1,
+};
+int rt_set_shard_mode(int mode);
 
 /* Environment-map importance sampling for next event estimation; 0 (default) = off.
  * The reference builds a luma CDF over 32 x 32 tiles of the environment map

@@ -5,7 +5,8 @@ accumulation buffer.  Two progressive frames are rendered, and rank 1 starts wit
 its accumulation buffer: the result must equal the single-rank accumulation of both frames up
 to float summation order, and rank 1's buffer must be left untouched.
 
-The CPU test renders the shards with the oracle; the GPU test renders them with the HIP path
+The CPU test renders the shards with the oracle; the GPU tests render them with the HIP path, by
+tiles and by sample passes (RT_SHARD_PASSES, bench.py's default)
 (rt_render_device into a torch tensor on cuda:0, both ranks on the one GPU of the box) and
 reduces with gloo on host copies (RCCL cannot put two ranks on one device).
 """
@@ -44,7 +45,9 @@ def _worker(rank, world, port, out_path, backend):
     accum = torch.zeros((H, W, 4), dtype=torch.float32)
     if rank:
         accum.fill_(123.0)                 # a rank other than 0 never reads or changes its buffer
-    dev = rt.DeviceScene(scene, 0) if backend == "gpu" else None
+    dev = rt.DeviceScene(scene, 0) if backend.startswith("gpu") else None
+    if backend == "gpu_passes":             # bench.py's default: each rank a range of the sample passes
+        rt.set_shard_mode(rt.abi.RT_SHARD_PASSES)
     frame = {"fc": 0, "tfi": 0}
 
     def render_shard(shard_index, shard_count, buf):
@@ -75,6 +78,7 @@ def _worker(rank, world, port, out_path, backend):
         assert torch.all(accum == 123.0)
     assert len(owned_tiles(W, H, 64, 64, rank, world)) >= 1
     if dev is not None:
+        rt.set_shard_mode(rt.abi.RT_SHARD_TILES)
         dev.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -117,3 +121,8 @@ def test_owned_tiles_partition(rt):
     for world in (1, 2, 3, 8):
         tiles = sorted(t for r in range(world) for t in owned_tiles(1920, 1080, 64, 64, r, world))
         assert tiles == list(range(30 * 17))
+
+
+@pytest.mark.gpu
+def test_two_rank_gloo_hip_pass_shards_match_single(rt, tmp_path):
+    _run(rt, tmp_path, "gpu_passes")

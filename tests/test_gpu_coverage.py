@@ -190,3 +190,40 @@ def test_sharded_frames_sum(rt, n, mode):
     assert sum(p[1].samples for p in parts) == fs.samples
     assert sum(p[1].closest_hit_rays for p in parts) == fs.closest_hit_rays
     assert rel_l2(total, full) <= 1e-5
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("mode", ["stream", "atomic"])
+def test_pass_sharded_frames_sum(rt, n, mode):
+    """RT_SHARD_PASSES: shard i of n renders every tile over sample passes [spp*i/n, spp*(i+1)/n).
+    The shares sum to the single-rank frame (same sample keys, so the same samples and rays, only
+    the float sums regrouped), including a pass count that does not divide evenly (n = 3), and an
+    exact-splat request renders as the streaming splat."""
+    scene, cam, st, fc, post = rt.load_preset("c3", 320, 200)
+    st.samples_per_pixel = 16
+    m = rt.abi.RT_SPLAT_ATOMIC if mode == "atomic" else rt.abi.RT_SPLAT_STREAM
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        with rt.splat_mode(m):
+            full, fs = dev.render(cam, st, fc, 320, 200)
+            rt.set_shard_mode(rt.abi.RT_SHARD_PASSES)
+            try:
+                parts = [dev.render(cam, st, fc, 320, 200, shard_index=r, shard_count=n) for r in range(n)]
+            finally:
+                rt.set_shard_mode(rt.abi.RT_SHARD_TILES)
+        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+            rt.set_shard_mode(rt.abi.RT_SHARD_PASSES)
+            try:
+                ex, es = dev.render(cam, st, fc, 320, 200, shard_index=0, shard_count=n)
+            finally:
+                rt.set_shard_mode(rt.abi.RT_SHARD_TILES)
+    finally:
+        dev.close()
+    total = sum(p[0].astype(np.float64) for p in parts)
+    REPORT[f"pass_sharded_{mode}_{n}"] = {"rel_l2": rel_l2(total, full), "samples": [int(p[1].samples) for p in parts]}
+    assert [p[1].samples for p in parts] == [320 * 200 * (16 * (r + 1) // n - 16 * r // n) for r in range(n)]
+    assert sum(p[1].closest_hit_rays for p in parts) == fs.closest_hit_rays
+    assert sum(p[1].shadow_rays for p in parts) == fs.shadow_rays
+    assert rel_l2(total, full) <= (1e-5 if mode == "stream" else 1e-4)
+    assert es.splat_mode == rt.abi.RT_SPLAT_STREAM
+    assert np.array_equal(ex, parts[0][0]) or mode == "atomic"
