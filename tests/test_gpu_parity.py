@@ -412,3 +412,26 @@ def test_fused_drain_matches_separate_kernels(which, w, h, spp, request, monkeyp
         assert np.array_equal(sm, ref[1]), name
         assert np.array_equal(samp, ref[2]), name
     assert out["all"][4] < out["off"][4]          # the fused drain ended the frame in fewer iterations
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2])
+def test_fused_drain_shallow_paths(c1, depth, monkeypatch):
+    """max_bounce_count 0 (nothing traced: every path finished at generation), 1 and 2: the fused
+    drain gives the separate kernels' frame and ray counts, and the oracle's frame."""
+    rt, scene, cam, st, fc, dev = c1
+    st = type(st).from_buffer_copy(st)
+    st.max_bounce_count = depth
+    st.samples_per_pixel = 8
+    out = []
+    for val in ("0", "1000000000"):
+        monkeypatch.setenv("RT_FUSE_PATHS", val)
+        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+            out.append(dev.render(cam, st, fc, 256, 256))
+    cpu, cs = ob.render(scene.desc(), cam, st, fc, 256, 256, rng_mode=0, threads=1)
+    (a, as_), (b, bs) = out
+    REPORT[f"fused_drain_depth{depth}"] = {"frames_equal": bool(np.array_equal(a, b)),
+                                          "oracle_pixels_bit_identical": float(np.all(b == cpu, axis=2).mean())}
+    assert np.array_equal(a, b)
+    assert (as_.closest_hit_rays, as_.shadow_rays) == (bs.closest_hit_rays, bs.shadow_rays) == \
+        (cs.closest_hit_rays, cs.shadow_rays)
+    assert np.all(b == cpu, axis=2).mean() >= 0.999
