@@ -2232,14 +2232,22 @@ __global__ void __launch_bounds__(BLOCK) k_drain_list(Pool pool, Counters* cnt) 
 // k_drain — the rest of every live path (see above).  Persistent waves fetch CHUNK slots of
 // the list per atomic, like k_trace.  Ray counts as the separate kernels make them: a closest
 // ray per continuation, a shadow ray per NEE cast, "traced" for the rays that enter a BVH.
+// One wave per block (DTB): a launch that finds the flag unset still has every block dispatched, and a
+// ~220-VGPR wave finds room on one SIMD much sooner than a 256-thread block does on four at once beside
+// the other partitions' kernels (those empty launches cost up to ~1 ms each in the iterations before
+// the drain).
+#ifndef RT_DRAIN_TB
+#define RT_DRAIN_TB 64
+#endif
+constexpr int DTB = RT_DRAIN_TB;
 template <bool LST, bool ENV>
-__global__ void __launch_bounds__(TB) k_drain(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
-                                              uint2* spill) {
+__global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
+                                               uint2* spill) {
     if (!cnt->fused || cnt->done) return;                              // uniform
-    __shared__ uint2 lds_stack[STACK_LDS*TB];
+    __shared__ uint2 lds_stack[STACK_LDS*DTB];
     Stack stk;
-    stk.lds = lds_stack; stk.spill = spill; stk.lane = threadIdx.x; stk.block = TB;
-    stk.gtid = blockIdx.x*TB + threadIdx.x; stk.nthreads = gridDim.x*TB;
+    stk.lds = lds_stack; stk.spill = spill; stk.lane = threadIdx.x; stk.block = DTB;
+    stk.gtid = blockIdx.x*DTB + threadIdx.x; stk.nthreads = gridDim.x*DTB;
     __shared__ uint32_t qlen[NSHARD];
     if (threadIdx.x < NSHARD) qlen[threadIdx.x] = cnt->drain_count[threadIdx.x][0];
     __syncthreads();
@@ -3327,7 +3335,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     // 8: 1x 40.5 ms, 2.5x 39.3 ms, 4.5x 40.0 ms, 9x 41.0 ms); RT_FUSE_PATHS another count (0 = never), read
     // per frame
     const char* fz = getenv("RT_FUSE_PATHS");
-    const uint32_t fuse_paths = fz ? (uint32_t)strtoul(fz, nullptr, 10) : s->drain_grid*TB*5u/2u;
+    const uint32_t fuse_paths = fz ? (uint32_t)strtoul(fz, nullptr, 10) : s->drain_grid*DTB*5u/2u;
     for (int k = 0; k < nparts; ++k) {
         int err = ensure_partition(s, k);
         if (!err) err = ensure_pool(s->part[k], pool_n);
@@ -3427,11 +3435,11 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if (fuse) {
             k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
             if (s->ds.listed_only) {
-                if (env) k_drain<true, true><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-                else k_drain<true, false><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                if (env) k_drain<true, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<true, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
             } else {
-                if (env) k_drain<false, true><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-                else k_drain<false, false><<<s->drain_grid, TB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                if (env) k_drain<false, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<false, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
             }
         }
         b(RT_KERNEL_EXTEND);
@@ -4001,9 +4009,10 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         s->connect_grid = std::min(s->trace_grid,
                                    std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)connect_pct / 100ull)));
         int drain_cu = 0;     // k_drain holds ~220 VGPRs: 2 waves per SIMD; its grid is what fits at once
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&drain_cu, k_drain<false, false>, TB, 0) != hipSuccess || drain_cu < 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&drain_cu, k_drain<false, false>, DTB, 0) != hipSuccess || drain_cu < 1)
             drain_cu = 1;
-        s->drain_grid = std::min(s->trace_grid, (uint32_t)(prop.multiProcessorCount*drain_cu));
+        // (lanes <= the trace grid's: the spill area is sized for those)
+        s->drain_grid = std::min(s->trace_grid*(uint32_t)(TB / DTB), (uint32_t)(prop.multiProcessorCount*drain_cu));
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
