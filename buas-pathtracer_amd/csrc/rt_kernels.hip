@@ -3331,11 +3331,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     double kms[RT_KERNEL_COUNT] = {};
     uint64_t klaunch[RT_KERNEL_COUNT] = {};
     const uint32_t life = std::max<uint32_t>(st->max_bounce_count, 1u);
-    // live paths at which the drain is fused (k_drain): 2.5 times its grid's lanes (r02 sweep, rank 0 of
-    // 8: 1x 40.5 ms, 2.5x 39.3 ms, 4.5x 40.0 ms, 9x 41.0 ms); RT_FUSE_PATHS another count (0 = never), read
-    // per frame
+    // live paths at which the drain is fused (k_drain): 2.5 times its grid's lanes, or a tenth of the
+    // pool if more (r02 sweeps: rank 0 of 8, 3.3M-path pools: 1x the lanes 40.5 ms, 2.5x 39.3, 4.5x 40.0,
+    // 9x 41.0; the full frame's 8.4M-path pools: 2.5x 235.8, 600k 234.1-235.2, 1M 234.2-234.3 ms);
+    // RT_FUSE_PATHS another count (0 = never), read per frame
     const char* fz = getenv("RT_FUSE_PATHS");
-    const uint32_t fuse_paths = fz ? (uint32_t)strtoul(fz, nullptr, 10) : s->drain_grid*DTB*5u/2u;
+    const uint32_t fuse_paths = fz ? (uint32_t)strtoul(fz, nullptr, 10)
+                                   : std::max(s->drain_grid*DTB*5u/2u, pool_n / 10u);
     for (int k = 0; k < nparts; ++k) {
         int err = ensure_partition(s, k);
         if (!err) err = ensure_pool(s->part[k], pool_n);
