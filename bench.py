@@ -73,13 +73,35 @@ def import_package():
     return mod
 
 
+def host_cores():
+    """The cores this process may run on: the affinity mask, capped by the cgroup CPU quota (a GPU
+    box shows the whole machine in os.cpu_count() but grants each GPU a share of it)."""
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = nproc
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    cores = affinity if quota is None else max(1, min(affinity, int(quota + 0.5)))
+    return {"cores": cores, "nproc": nproc, "affinity": affinity, "cgroup_quota_cores": quota}
+
+
 def cpu_baseline(rt, cfg, spp_override, seconds_budget=15.0):
-    """Oracle (C restatement, reference-stream RNG, tile queue) on a bounded tile sample."""
+    """Oracle (C restatement, reference-stream RNG, tile queue) on a bounded tile sample, at the
+    box's core count N and at the reference's own 1.25 N worker threads (RT/raytracer.cpp:1580-1592)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_binding as ob
     lib = ob.load()
-    threads = int(os.environ.get("RT_CPU_THREADS", min(16, os.cpu_count() or 1)))
+    hc = host_cores()
+    threads = int(os.environ.get("RT_CPU_THREADS", hc["cores"]))
     scene, cam, st, fc, post = rt.load_preset(cfg["preset"], cfg["w"], cfg["h"], asset_dir=None)
     if spp_override:
         st.samples_per_pixel = spp_override
@@ -108,11 +130,19 @@ def cpu_baseline(rt, cfg, spp_override, seconds_budget=15.0):
     tiles = [(k * step + step // 2) % total_tiles for k in range(n_tiles)]
     dt, stats = run(tiles, threads)
     rays = stats.closest_hit_rays + stats.shadow_rays
+    # the reference's worker count, 1.25 x the cores (RT/raytracer.cpp:1588), on the same tiles
+    t125 = max(1, int(threads * 1.25))
+    dt125, stats125 = run(tiles, t125)
+    rays125 = stats125.closest_hit_rays + stats125.shadow_rays
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "samples_per_s": stats.samples / dt,
+            "host": hc,
+            "threads_1p25": {"threads": t125, "value": rays125 / dt125 / 1e6, "samples_per_s": stats125.samples / dt125,
+                             "seconds": round(dt125, 2)},
             "sample": f"{n_tiles} of {total_tiles} 64x64 tiles (evenly spaced) of the same {w}x{h} "
-                      f"{st.samples_per_pixel}spp frame, reference-stream RNG, {threads} threads, "
-                      f"{dt:.1f} s, {rays} rays"}
+                      f"{st.samples_per_pixel}spp frame, reference-stream RNG, {threads} threads "
+                      f"(the box's cores: affinity {hc['affinity']}, cgroup quota {hc['cgroup_quota_cores']}, "
+                      f"nproc {hc['nproc']}), {dt:.1f} s, {rays} rays; again at {t125} threads"}
 
 
 def main():
@@ -137,6 +167,14 @@ def main():
     ap.add_argument("--env-sampling", type=int, default=0,
                     help="1: environment-map NEE (rt_set_env_sampling; beyond the reference's estimator)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL over xGMI, the product path) or gloo (framebuffer reduced through host "
+                         "memory: lets several ranks share one GPU in the tests)")
+    ap.add_argument("--c4-steps", type=int, default=5,
+                    help="also time the north star's own scene (C4, 1080p 256 spp) for this many frames "
+                         "after one warm-up frame, same ranks and sharding (0 = skip)")
+    ap.add_argument("--dump-frame", default="",
+                    help="rank 0 saves the accumulated frame of the last timed step (.npy; tests)")
     args = ap.parse_args()
 
     import torch
@@ -146,12 +184,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    # one GPU per rank; ranks beyond the visible GPUs share them (gloo tests on a 1-GPU box)
+    device = local_rank % max(1, torch.cuda.device_count())
     if distributed:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    device = local_rank
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
     torch.cuda.set_device(device)
+    # the ray / time totals go through the backend's own memory (gloo reduces host tensors)
+    red_dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{device}"
 
     rt = import_package()
     cfg = dict(CONFIGS[args.config])
@@ -160,36 +201,40 @@ def main():
     if args.height:
         cfg["h"] = args.height
     w, h = cfg["w"], cfg["h"]
-    asset_dir = os.path.join(ROOT, "gpurun_out", "assets") if os.path.isdir(os.path.join(ROOT, "gpurun_out")) else None
-    if asset_dir:
+    # Synthetic assets go through their files (the OBJ / RGBE parsers) on one rank only; ranks
+    # started together build them in memory, so none can read another's file mid-write.
+    asset_dir = None
+    if world == 1 and os.path.isdir(os.path.join(ROOT, "gpurun_out")):
+        asset_dir = os.path.join(ROOT, "gpurun_out", "assets")
         os.makedirs(asset_dir, exist_ok=True)
-    scene, cam, st, fc, post = rt.load_preset(cfg["preset"], w, h, asset_dir=asset_dir)
-    if args.spp:
-        st.samples_per_pixel = args.spp
-    if args.pool:
-        rt.lib().rt_set_path_pool(args.pool)
-    if args.env_sampling:
-        rt.set_env_sampling(args.env_sampling)
-    rt.set_shard_mode(rt.abi.RT_SHARD_PASSES if args.shard_mode == "passes" else rt.abi.RT_SHARD_TILES)
-    dev = rt.DeviceScene(scene, device)
-    accum = torch.zeros((h, w, 4), dtype=torch.float32, device=f"cuda:{device}")
+    shard_mode = rt.abi.RT_SHARD_PASSES if args.shard_mode == "passes" else rt.abi.RT_SHARD_TILES
     stream = torch.cuda.current_stream(device)
-
     from buas_pathtracer_amd.sharding import render_frame_sharded
 
-    def render_shard(shard_index, shard_count, buf):
-        return dev.render_device(cam, st, fc, w, h, buf.data_ptr(), stream=stream.cuda_stream,
-                                 shard_index=shard_index, shard_count=shard_count)
+    def setup(name, fw, fh, adir):
+        scene, cam, st, fc, post = rt.load_preset(CONFIGS[name]["preset"], fw, fh, asset_dir=adir)
+        dev = rt.DeviceScene(scene, device)
+        # per-scene settings (rt_scene_config): this scene's shard mode, pool and environment NEE
+        dev.configure(shard_mode=shard_mode, path_pool=args.pool, env_sampling=1 if args.env_sampling else 0)
+        accum = torch.zeros((fh, fw, 4), dtype=torch.float32, device=f"cuda:{device}")
+        scratch = torch.zeros_like(accum) if world > 1 else None
 
-    scratch = torch.zeros_like(accum) if world > 1 else None
+        def render_shard(shard_index, shard_count, buf):
+            return dev.render_device(cam, st, fc, fw, fh, buf.data_ptr(), stream=stream.cuda_stream,
+                                     shard_index=shard_index, shard_count=shard_count)
 
-    def step():
-        accum.zero_()
-        if args.shard_of > 1:                          # diagnostic: one rank's share of an N-rank frame
-            return render_shard(args.shard_index, args.shard_of, accum)
-        # tiles t % world == rank into a zeroed frame buffer, the RCCL sum-reduce of it over
-        # xGMI into rank 0, which adds it to its accumulation buffer
-        return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch)
+        def step():
+            accum.zero_()
+            if args.shard_of > 1:                          # diagnostic: one rank's share of an N-rank frame
+                return render_shard(args.shard_index, args.shard_of, accum)
+            # this rank's share into a zeroed frame buffer, the RCCL sum-reduce of it over xGMI into
+            # rank 0, which adds it to its accumulation buffer
+            return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch)
+        return scene, dev, st, post, accum, step
+
+    scene, dev, st, post, accum, step = setup(args.config, w, h, asset_dir)
+    if args.spp:
+        st.samples_per_pixel = args.spp
 
     # Warm-up frames time every stage (HIP events around each launch); the timed region
     # then records events for the dominant stage only, since each event pair is a queue
@@ -229,13 +274,51 @@ def main():
     elapsed = time.perf_counter() - t0
     rt.lib().rt_set_profiling(0)
 
-    totals = torch.tensor([closest, shadow, samples, traced, traced_sh], dtype=torch.float64, device=f"cuda:{device}")
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{device}")
+    totals = torch.tensor([closest, shadow, samples, traced, traced_sh], dtype=torch.float64, device=red_dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if distributed:
         dist.all_reduce(totals, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
     closest_all, shadow_all, samples_all, traced_all, traced_sh_all = [float(x) for x in totals.tolist()]
     elapsed = float(tmax.item())
+    if args.dump_frame and rank == 0:
+        import numpy as np
+        np.save(args.dump_frame, accum.cpu().numpy())
+
+    # The north star's own scene (BASELINE configs[3], C4: ~250k triangles, 1080p, 256 spp), timed on
+    # the same ranks with the same sharding: one warm-up frame, then --c4-steps frames.
+    c4 = None
+    if args.c4_steps > 0 and args.config != "c4" and args.shard_of <= 1:
+        c4scene, c4dev, c4st, _, c4acc, c4step = setup("c4", CONFIGS["c4"]["w"], CONFIGS["c4"]["h"], asset_dir)
+        c4step()
+        torch.cuda.synchronize(device)
+        if distributed:
+            dist.barrier()
+        c0 = time.perf_counter()
+        cr = [0, 0, 0]
+        for _ in range(args.c4_steps):
+            cs = c4step()
+            cr[0] += cs.closest_hit_rays
+            cr[1] += cs.shadow_rays
+            cr[2] += cs.samples
+        torch.cuda.synchronize(device)
+        if distributed:
+            dist.barrier()
+        ct = torch.tensor([time.perf_counter() - c0], dtype=torch.float64, device=red_dev)
+        crt = torch.tensor(cr, dtype=torch.float64, device=red_dev)
+        if distributed:
+            dist.all_reduce(crt, op=dist.ReduceOp.SUM)
+            dist.all_reduce(ct, op=dist.ReduceOp.MAX)
+        c4dev.close()
+        cel = float(ct.item())
+        c4_rays = float(crt[0]) + float(crt[1])
+        c4 = {"workload": f"c4: c4 {CONFIGS['c4']['w']}x{CONFIGS['c4']['h']} {c4st.samples_per_pixel}spp "
+                          f"depth {c4st.max_bounce_count} (~250k triangles, four meshes, nested dielectrics)",
+              "steps": args.c4_steps, "warmup": 1, "ms_per_step": round(1e3 * cel / args.c4_steps, 3),
+              "value": round(c4_rays / cel / 1e6, 3), "unit": "Mrays/s",
+              "samples_per_s": round(float(crt[2]) / cel, 1),
+              "samples_per_s_per_gpu": round(float(crt[2]) / cel / world, 1),
+              "closest_hit_rays": int(crt[0]), "shadow_rays": int(crt[1])}
 
     if rank == 0:
         rays = closest_all + shadow_all
@@ -312,6 +395,9 @@ def main():
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(rt, cfg, args.spp, args.cpu_seconds)
+        parallelism = (f"{args.shard_mode}%{args.shard_of} (rank {args.shard_index} only, diagnostic)"
+                       if args.shard_of > 1 else f"{args.shard_mode}%{world}" +
+                       (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_reduce" if world > 1 else ""))
         out = {
             "metric": METRIC,
             "value": round(mrays, 3),
@@ -336,7 +422,12 @@ def main():
                                    f"depth {st.max_bounce_count}" + (" env-sampling" if args.env_sampling else ""),
                        "width": w, "height": h,
                        "spp": st.samples_per_pixel, "max_depth": st.max_bounce_count,
-                       "parallelism": (f"{args.shard_mode}%{args.shard_of} (rank {args.shard_index} only, diagnostic)" if args.shard_of > 1 else f"{args.shard_mode}%{world}" + ("+rccl_reduce" if world > 1 else ""))},
+                       "parallelism": parallelism,
+                       "shard_mode": args.shard_mode,
+                       "shard_modes": "passes: rank r renders sample passes [spp*r/N, spp*(r+1)/N) of every tile "
+                                      "(default, equal cost per rank); tiles: tile t on rank t % N (the north "
+                                      "star's wording, --shard-mode tiles); both sum to the same frame "
+                                      "(DESIGN.md section 7)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "kernel": KERNEL[dom], "bytes_per_unit": BYTES_PER_UNIT[dom],
@@ -350,6 +441,7 @@ def main():
                                   enumerate(STAGES)},
             "stage_ms_note": ("HIP-event time per stage summed over its launches, from the warm-up frames "
                               "(4 partitions overlap, so the sum exceeds ms_per_step)"),
+            "c4": c4,
             "cpu_baseline": cpu,
             "postprocess": postprocess,
         }

@@ -168,8 +168,11 @@ class Scene:
         """triangles: float32 array [n,3,3]; normals: optional [n,3,3] (per-vertex)."""
         t = np.ascontiguousarray(triangles, dtype=np.float32).reshape(-1, 3, 3)
         n = None if normals is None else np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 3, 3)
-        return lib().rth_create_mesh(self._h, t.shape[0], t.ctypes.data_as(C.POINTER(V3)),
-                                     None if n is None else n.ctypes.data_as(C.POINTER(V3)), method)
+        mid = lib().rth_create_mesh(self._h, t.shape[0], t.ctypes.data_as(C.POINTER(V3)),
+                                    None if n is None else n.ctypes.data_as(C.POINTER(V3)), method)
+        if mid == 0xFFFFFFFF:
+            raise RuntimeError(f"rth_create_mesh failed: {(lib().rth_last_error() or b'').decode()}")
+        return mid
 
     def load_obj_mesh(self, path, method=abi.RTH_BVH_SAH_BINNED):
         out = C.c_uint32()
@@ -192,7 +195,8 @@ class Scene:
             raise ValueError(lib().rth_last_error().decode())
 
     def create_scene_bvh(self):
-        lib().rth_create_scene_bvh(self._h)
+        if not lib().rth_create_scene_bvh(self._h):
+            raise RuntimeError(f"rth_create_scene_bvh failed: {(lib().rth_last_error() or b'').decode()}")
 
     def bvh_info(self, mesh_id=None):
         info = BvhInfo()
@@ -279,6 +283,42 @@ class DeviceScene:
 
     def cancel(self):
         lib().rt_cancel(self._h)
+
+    def config(self):
+        """rt_scene_get_config: this scene's schedule and splat settings (abi.SceneConfig)."""
+        c = abi.SceneConfig()
+        _check(lib().rt_scene_get_config(self._h, C.byref(c)))
+        return c
+
+    def configure(self, **fields):
+        """rt_scene_set_config with the named fields changed, e.g. configure(partitions=1,
+        splat_mode=abi.RT_SPLAT_EXACT).  Returns the previous configuration (pass it to
+        set_config to restore it)."""
+        old = self.config()
+        c = abi.SceneConfig.from_buffer_copy(old)
+        for k, v in fields.items():
+            if k not in dict(abi.SceneConfig._fields_):
+                raise AttributeError(f"rt_scene_config has no field {k!r}")
+            setattr(c, k, v)
+        self.set_config(c)
+        return old
+
+    def set_config(self, c):
+        _check(lib().rt_scene_set_config(self._h, C.byref(c)))
+
+    def configured(self, **fields):
+        """with dev.configured(partitions=1): ... -- the scene's configuration restored after."""
+        dev = self
+
+        class _Ctx:
+            def __enter__(self):
+                self.old = dev.configure(**fields)
+                return dev
+
+            def __exit__(self, *exc):
+                dev.set_config(self.old)
+                return False
+        return _Ctx()
 
 
 def resolve_bgra8(accum, post):

@@ -149,6 +149,16 @@ class PostSettings(C.Structure):      # RT/scene.h:84-90
                 ("midpoint", C.c_float), ("contrast", C.c_float)]
 
 
+RT_CONFIG_INHERIT = -1
+
+
+class SceneConfig(C.Structure):       # rt_scene_config (per-scene schedule and splat settings)
+    _fields_ = [("splat_mode", C.c_int32), ("shard_mode", C.c_int32), ("env_sampling", C.c_int32),
+                ("partitions", C.c_int32), ("path_pool", C.c_int64), ("fuse_paths", C.c_int64),
+                ("splat_chunk", C.c_int32), ("splat_ring", C.c_int32), ("sample_budget_gb", C.c_double),
+                ("resolve_tall_pixels", C.c_int64), ("debug_traversal", C.c_int32), ("reserved", C.c_int32 * 7)]
+
+
 class BvhInfo(C.Structure):
     _fields_ = [("node_count", C.c_uint32), ("leaf_count", C.c_uint32), ("max_depth", C.c_uint32),
                 ("max_leaf_size", C.c_uint32)]
@@ -187,6 +197,9 @@ ABI_FUNCTIONS = {
     "rt_render_picture": (C.c_int, [C.c_void_p, P(Camera), P(Settings), P(FilterCache), P(TileSet), C.c_uint32,
                                     C.c_uint32, C.c_uint32, P(PostSettings), P(C.c_uint32), P(Stats)]),
     "rt_cancel": (C.c_int, [C.c_void_p]),
+    "rt_scene_default_config": (C.c_int, [P(SceneConfig)]),
+    "rt_scene_get_config": (C.c_int, [C.c_void_p, P(SceneConfig)]),
+    "rt_scene_set_config": (C.c_int, [C.c_void_p, P(SceneConfig)]),
     "rt_postprocess_device": (C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, P(PostSettings), C.c_uint32,
                                         C.c_void_p, C.c_void_p]),
     "rt_postprocess": (C.c_int, [C.c_int, P(AccumulationBuffer), P(PostSettings), C.c_uint32, P(C.c_uint32)]),

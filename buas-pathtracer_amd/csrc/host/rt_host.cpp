@@ -732,7 +732,9 @@ int rth_load_obj_mesh(rth_scene* s, const char* path, int32_t method, uint32_t* 
     std::vector<rt_v3> tris, nrm;
     if (!parse_obj(file.data(), tris, nrm)) return 0;
     if (tris.empty()) { set_err("OBJ has no triangles"); return 0; }
-    *out = rth_create_mesh(s, (uint32_t)(tris.size()/3), tris.data(), nrm.empty() ? nullptr : nrm.data(), method);
+    const uint32_t id = rth_create_mesh(s, (uint32_t)(tris.size()/3), tris.data(), nrm.empty() ? nullptr : nrm.data(), method);
+    if (id == 0xFFFFFFFFu) return 0;               // the BVH build failed (rth_last_error says why)
+    *out = id;
     return 1;
 }
 
@@ -986,7 +988,7 @@ int rth_write_synthetic_obj(const char* path, uint32_t target, uint32_t seed) {
     for (auto& v : n) fprintf(f, "vn %.9g %.9g %.9g\n", v.x, v.y, v.z);
     for (size_t i = 0; i < t.size()/3; ++i)
         fprintf(f, "f %zu//%zu %zu//%zu %zu//%zu\n", 3*i + 1, 3*i + 1, 3*i + 2, 3*i + 2, 3*i + 3, 3*i + 3);
-    fclose(f);
+    if (fclose(f) != 0) { set_err(std::string("cannot write ") + path); return 0; }
     return 1;
 }
 
@@ -1020,7 +1022,7 @@ int rth_write_synthetic_hdr(const char* path, uint32_t w, uint32_t h, uint32_t s
     FILE* f = fopen(path, "wb");
     if (!f) { set_err(std::string("cannot write ") + path); return 0; }
     fwrite(out.data(), 1, out.size(), f);
-    fclose(f);
+    if (fclose(f) != 0) { set_err(std::string("cannot write ") + path); return 0; }
     return 1;
 }
 

@@ -10,6 +10,8 @@
 #include <string>
 #include <vector>
 #include <sys/stat.h>
+#include <unistd.h>
+#include <atomic>
 
 std::vector<uint8_t> rth_synthetic_hdr_bytes(uint32_t w, uint32_t h, uint32_t seed);
 int rth_load_environment_map_bytes(rth_scene* s, std::vector<char>& file);
@@ -65,13 +67,24 @@ struct Ctx {
 
 bool exists(const std::string& p) { struct stat st; return stat(p.c_str(), &st) == 0; }
 
+// A synthetic asset is written under a name private to this process and call, then renamed into
+// place: rename() within a directory is atomic, so a process that finds the file (ranks started
+// together sharing an asset directory) never parses a half-written one.
+template <class W>
+void write_asset(const std::string& path, W write) {
+    static std::atomic<uint32_t> seq{0};
+    const std::string tmp = path + ".tmp." + std::to_string((long)getpid()) + "." + std::to_string(seq++);
+    if (write(tmp.c_str()) && rename(tmp.c_str(), path.c_str()) == 0) return;
+    remove(tmp.c_str());                  // the caller then finds no file and builds the asset in memory
+}
+
 // load_mesh (RT/raytracer.cpp:148-158) with the synthetic stand-in for dragon_mcguire.obj.
 // The presets build the mesh BVH with binned SAH (the north star's SAH BVH);
 // the reference's load_mesh used BVH_MidpointSplit (:154).
 uint32_t load_mesh(Ctx& c, uint32_t triangles, uint32_t seed) {
     if (!c.asset_dir.empty()) {
         std::string path = c.asset_dir + "/synthetic_mesh_" + std::to_string(triangles) + "_s" + std::to_string(seed) + ".obj";
-        if (!exists(path)) rth_write_synthetic_obj(path.c_str(), triangles, seed);
+        if (!exists(path)) write_asset(path, [&](const char* f) { return rth_write_synthetic_obj(f, triangles, seed) != 0; });
         uint32_t id;
         if (rth_load_obj_mesh(c.s, path.c_str(), RTH_BVH_SAH_BINNED, &id)) return id;
     }
@@ -86,7 +99,7 @@ void load_env(Ctx& c, uint32_t seed) {
     const uint32_t W = 2048, H = 1024;
     if (!c.asset_dir.empty()) {
         std::string path = c.asset_dir + "/synthetic_sky_s" + std::to_string(seed) + ".hdr";
-        if (!exists(path)) rth_write_synthetic_hdr(path.c_str(), W, H, seed);
+        if (!exists(path)) write_asset(path, [&](const char* f) { return rth_write_synthetic_hdr(f, W, H, seed) != 0; });
         if (rth_load_environment_map(c.s, path.c_str())) return;
     }
     std::vector<uint8_t> b = rth_synthetic_hdr_bytes(W, H, seed);

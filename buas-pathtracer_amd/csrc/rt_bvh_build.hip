@@ -357,6 +357,8 @@ int rt_build_bvh(int device, uint32_t n, const rt_v3* p, const rt_v3* r, int met
         hp[i] = make_float4(p[i].x, p[i].y, p[i].z, f);
         hr[i] = make_float4(r[i].x, r[i].y, r[i].z, 0.0f);
     }
+    int prev_device = -1;                       // the caller's current device, restored at done
+    if (hipGetDevice(&prev_device) != hipSuccess) prev_device = -1;
     BVH_OK(hipSetDevice(device));
     BVH_OK(hipMalloc(&d_p, sizeof(float4)*n));
     BVH_OK(hipMalloc(&d_r, sizeof(float4)*n));
@@ -409,6 +411,7 @@ int rt_build_bvh(int device, uint32_t n, const rt_v3* p, const rt_v3* r, int met
 done:
     (void)hipFree(d_p); (void)hipFree(d_r); (void)hipFree(d_nodes); (void)hipFree(d_a); (void)hipFree(d_b);
     (void)hipFree(d_cnt); (void)hipFree(d_rank); (void)hipFree(d_order); (void)hipFree(d_out);
+    if (prev_device >= 0 && prev_device != device) (void)hipSetDevice(prev_device);
     return err;
 }
 

@@ -2993,6 +2993,7 @@ struct rt_scene {
     } layout;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
+    rt_scene_config cfg = {};           // rt_scene_set_config; read at every frame, never the environment
 };
 
 namespace {
@@ -3259,12 +3260,11 @@ struct FrameShape { int nparts; uint32_t pool_n; };
 #ifndef RT_POOL_DIV
 #define RT_POOL_DIV 5ull
 #endif
-FrameShape frame_shape(unsigned long long total, uint32_t passes) {
+FrameShape frame_shape(const rt_scene* s, unsigned long long total, uint32_t passes) {
     FrameShape f;
-    f.nparts = 4;
-    if (const char* e = getenv("RT_PARTITIONS")) f.nparts = std::max(1, std::min(MAX_PARTITIONS, atoi(e)));
+    f.nparts = s->cfg.partitions > 0 ? std::min(MAX_PARTITIONS, (int)s->cfg.partitions) : 4;
     if (passes) f.nparts = std::max(1, std::min<int>(f.nparts, (int)passes));   // partitions own whole passes
-    uint32_t pool_n = g_pool_override;
+    uint32_t pool_n = s->cfg.path_pool > 0 ? (uint32_t)s->cfg.path_pool : g_pool_override;
     if (!pool_n) {
         const unsigned long long want = total / (unsigned long long)f.nparts / RT_POOL_DIV;
         pool_n = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>(want, 1ull << 21), 4ull << 21);
@@ -3314,13 +3314,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
               const SplatCfg& sp, rt_stats* stats) {
     auto t0 = std::chrono::steady_clock::now();
     const bool listed = fp.list_xy != nullptr;
-    const FrameShape shape = frame_shape(total, listed ? 0u : sp.passes);
+    const FrameShape shape = frame_shape(s, total, listed ? 0u : sp.passes);
     const int nparts = shape.nparts;
     const uint32_t pool_n = shape.pool_n;
     const bool stream_splat = !listed && sp.mode == RT_SPLAT_STREAM;
     const size_t npx = (size_t)fp.w*fp.h;
     const uint32_t prof = g_profiling & ~(1u << RT_KERNEL_SPLAT);   // the splat runs inside k_generate
-    const int diag = getenv("RT_DEBUG_TRAVERSAL") ? 1 : 0;
+    const int diag = s->cfg.debug_traversal ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(s->start_ev, stream));
     struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live, drain, near;
@@ -3334,10 +3334,10 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     // live paths at which the drain is fused (k_drain): 2.5 times its grid's lanes, or a tenth of the
     // pool if more (r02 sweeps: rank 0 of 8, 3.3M-path pools: 1x the lanes 40.5 ms, 2.5x 39.3, 4.5x 40.0,
     // 9x 41.0; the full frame's 8.4M-path pools: 2.5x 235.8, 600k 234.1-235.2, 1M 234.2-234.3 ms);
-    // RT_FUSE_PATHS another count (0 = never), read per frame
-    const char* fz = getenv("RT_FUSE_PATHS");
-    const uint32_t fuse_paths = fz ? (uint32_t)strtoul(fz, nullptr, 10)
-                                   : std::max(s->drain_grid*DTB*5u/2u, pool_n / 10u);
+    // rt_scene_config::fuse_paths another count (0 = never)
+    const uint32_t fuse_paths = s->cfg.fuse_paths >= 0
+        ? (uint32_t)std::min<int64_t>(s->cfg.fuse_paths, 0xFFFFFFFFll)
+        : std::max(s->drain_grid*DTB*5u/2u, pool_n / 10u);
     for (int k = 0; k < nparts; ++k) {
         int err = ensure_partition(s, k);
         if (!err) err = ensure_pool(s->part[k], pool_n);
@@ -3418,7 +3418,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         }
     };
     // environment-map NEE (rt_set_env_sampling): only with a map, its table and NEE
-    const bool env = g_env_sampling && s->ds.env_tab && st->next_event_estimation;
+    const bool env = (s->cfg.env_sampling >= 0 ? s->cfg.env_sampling : g_env_sampling) && s->ds.env_tab &&
+                     st->next_event_estimation;
     auto iterate = [&](int k, bool plan) {
         Partition& pt = s->part[k];
         Run& r = run[k];
@@ -3688,9 +3689,68 @@ bool build_env_table(uint32_t w, uint32_t h, const rt_v3* px, std::vector<float4
     return true;
 }
 
+rt_scene_config default_config() {
+    rt_scene_config c;
+    memset(&c, 0, sizeof(c));
+    c.splat_mode = RT_CONFIG_INHERIT;
+    c.shard_mode = RT_CONFIG_INHERIT;
+    c.env_sampling = RT_CONFIG_INHERIT;
+    c.fuse_paths = -1;
+    c.sample_budget_gb = -1.0;
+    return c;
+}
+
+int check_config(const rt_scene_config* c) {
+    const char* bad = nullptr;
+    if (c->splat_mode != RT_CONFIG_INHERIT && (c->splat_mode < RT_SPLAT_STREAM || c->splat_mode > RT_SPLAT_ATOMIC)) bad = "splat_mode";
+    else if (c->shard_mode != RT_CONFIG_INHERIT && c->shard_mode != RT_SHARD_TILES && c->shard_mode != RT_SHARD_PASSES) bad = "shard_mode";
+    else if (c->env_sampling != RT_CONFIG_INHERIT && c->env_sampling != 0 && c->env_sampling != 1) bad = "env_sampling";
+    else if (c->partitions < 0 || c->partitions > MAX_PARTITIONS) bad = "partitions (0..8)";
+    else if (c->path_pool < 0 || c->path_pool > (1ll << 30)) bad = "path_pool (0..2^30)";
+    else if (c->fuse_paths < -1) bad = "fuse_paths";
+    else if (c->splat_chunk < 0 || c->splat_ring < 0) bad = "splat_chunk / splat_ring";
+    else if (!(c->sample_budget_gb == c->sample_budget_gb)) bad = "sample_budget_gb";
+    else if (c->resolve_tall_pixels < 0) bad = "resolve_tall_pixels";
+    if (bad) { set_error(std::string("rt_scene_config: bad ") + bad); return RT_ERROR_INVALID; }
+    return RT_OK;
+}
+
+// The test-override environment variables, applied once at rt_scene_upload (never per frame).
+void config_from_env(rt_scene_config& c) {
+    if (const char* e = getenv("RT_SPLAT")) c.splat_mode = atoi(e);
+    if (const char* e = getenv("RT_PARTITIONS")) c.partitions = std::max(1, std::min(MAX_PARTITIONS, atoi(e)));
+    if (const char* e = getenv("RT_FUSE_PATHS")) c.fuse_paths = (int64_t)strtoull(e, nullptr, 10);
+    if (const char* e = getenv("RT_SPLAT_CHUNK")) c.splat_chunk = std::max(1, atoi(e));
+    if (const char* e = getenv("RT_SPLAT_RING")) c.splat_ring = std::max(1, atoi(e));
+    if (const char* e = getenv("RT_SAMPLE_BUDGET_GB")) c.sample_budget_gb = std::max(0.0, atof(e));
+    if (const char* e = getenv("RT_RES_TALL_PIXELS")) c.resolve_tall_pixels = (int64_t)strtoull(e, nullptr, 0);
+    if (getenv("RT_DEBUG_TRAVERSAL")) c.debug_traversal = 1;
+}
+
 }  // namespace
 
 extern "C" {
+
+int rt_scene_default_config(rt_scene_config* out) {
+    if (!out) { set_error("null argument"); return RT_ERROR_INVALID; }
+    *out = default_config();
+    return RT_OK;
+}
+
+int rt_scene_get_config(const rt_scene* s, rt_scene_config* out) {
+    if (!s || !out) { set_error("null argument"); return RT_ERROR_INVALID; }
+    *out = s->cfg;
+    return RT_OK;
+}
+
+int rt_scene_set_config(rt_scene* s, const rt_scene_config* c) {
+    if (!s || !c) { set_error("null argument"); return RT_ERROR_INVALID; }
+    int err = check_config(c);
+    if (err) return err;
+    s->cfg = *c;
+    memset(s->cfg.reserved, 0, sizeof(s->cfg.reserved));
+    return RT_OK;
+}
 
 int rt_abi_version(void) { return RT_ABI_VERSION; }
 const char* rt_last_error(void) { return g_error.c_str(); }
@@ -3731,6 +3791,9 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     if (d->material_count == 0 || d->material_count >= 0xFFFFu) { set_error("material count must be in [1, 65534]"); return RT_ERROR_INVALID; }
     rt_scene* s = new rt_scene();
     s->device = device;
+    s->cfg = default_config();
+    config_from_env(s->cfg);
+    if ((err = check_config(&s->cfg))) { delete s; return err; }
     DevScene& ds = s->ds;
     auto fail = [&](int e) { rt_scene_free(s); return e; };
     // materials + the integrator's local `air` (RT/integrators.cpp:597-599)
@@ -4107,7 +4170,8 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     uint32_t tcy = (h + tiles->tile_h - 1) / tiles->tile_h;
     if (w > 65535 || h > 65535) { set_error("frame larger than 65535 pixels a side"); return RT_ERROR_INVALID; }
     // RT_SHARD_PASSES: every tile, and the shard's range of sample passes (below)
-    const bool by_pass = g_shard_mode == RT_SHARD_PASSES && tiles->shard_count > 1;
+    const int shard_mode = s->cfg.shard_mode >= 0 ? s->cfg.shard_mode : g_shard_mode;
+    const bool by_pass = shard_mode == RT_SHARD_PASSES && tiles->shard_count > 1;
     const uint32_t tsi = by_pass ? 0u : tiles->shard_index, tsc = by_pass ? 1u : tiles->shard_count;
     auto& L = s->layout;
     const bool same = L.valid && L.w == w && L.h == h && L.tw == tiles->tile_w && L.th == tiles->tile_h &&
@@ -4192,10 +4256,10 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     // one pass per partition does not fit.
     const uint32_t spp = pass_hi - pass_lo;                       // this shard's passes
     const int ks = fp.cache_size ? fp.kernel_size : 0;
-    const FrameShape shape = frame_shape(total, spp);
-    int want_mode = g_splat_mode;
-    if (const char* e = getenv("RT_SPLAT")) want_mode = atoi(e);
-    if (by_pass && want_mode == RT_SPLAT_EXACT) want_mode = RT_SPLAT_STREAM;   // k_resolve gathers passes 0..spp-1
+    const FrameShape shape = frame_shape(s, total, spp);
+    int want_mode = s->cfg.splat_mode >= 0 ? s->cfg.splat_mode : g_splat_mode;
+    // k_resolve gathers passes 0..spp-1 of one record array: a pass shard never takes the exact splat
+    if (by_pass && want_mode == RT_SPLAT_EXACT) want_mode = RT_SPLAT_STREAM;
     // the splat for a record budget (bytes): the mode, and for STREAM the ring and chunk
     auto plan_splat = [&](double budget, SplatCfg& sp, size_t& need_rec) {
         sp = SplatCfg{};
@@ -4204,7 +4268,10 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         sp.mode = want_mode;
         need_rec = 0;
         if (sp.mode == RT_SPLAT_EXACT && (double)total*20.0 > budget) sp.mode = RT_SPLAT_STREAM;
-        if (sp.mode == RT_SPLAT_STREAM && ks > 12) sp.mode = (double)total*20.0 <= budget ? RT_SPLAT_EXACT : RT_SPLAT_ATOMIC;
+        // past the radius k_resolve_tiles stages: the exact gather, or atomics for a pass shard (whose
+        // records would be placed at pass_lo*P in an array sized for its own passes) or over budget
+        if (sp.mode == RT_SPLAT_STREAM && ks > 12)
+            sp.mode = (!by_pass && (double)total*20.0 <= budget) ? RT_SPLAT_EXACT : RT_SPLAT_ATOMIC;
         if (sp.mode == RT_SPLAT_STREAM) {
             // a resolve every ~32M samples, and at least four per partition (a small shard, e.g. one
             // rank's eighth of a frame, would otherwise resolve all its passes after its drain); the
@@ -4213,10 +4280,10 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
             const uint32_t per_part = (spp + shape.nparts - 1) / shape.nparts;
             sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull),
                                                                std::max(1u, per_part / 4));
-            if (const char* e = getenv("RT_SPLAT_CHUNK")) sp.chunk = std::max(1, atoi(e));
+            if (s->cfg.splat_chunk > 0) sp.chunk = (uint32_t)s->cfg.splat_chunk;
             const unsigned long long lag = (5ull*shape.pool_n + fp.pixels - 1) / fp.pixels;
             sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, per_part);
-            if (const char* e = getenv("RT_SPLAT_RING")) sp.ring = std::max(1, atoi(e));
+            if (s->cfg.splat_ring > 0) sp.ring = (uint32_t)s->cfg.splat_ring;
             sp.chunk = std::min(sp.chunk, sp.ring);                   // the planner needs chunk <= ring
             while (sp.ring > 1 && 20.0*(double)shape.nparts*sp.ring*fp.pixels > budget) {
                 sp.ring = std::max(1u, sp.ring / 2);
@@ -4230,9 +4297,9 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     // The records held already need no budget: the free-memory query runs only when they must grow.
     SplatCfg sp;
     size_t need_rec = 0;
-    const char* bud_env = getenv("RT_SAMPLE_BUDGET_GB");
-    plan_splat(bud_env ? atof(bud_env)*1e9 : 20.0*(double)s->samp_cap, sp, need_rec);
-    if (!bud_env && (sp.mode != want_mode || need_rec > s->samp_cap)) {
+    const bool fixed_budget = s->cfg.sample_budget_gb >= 0.0;
+    plan_splat(fixed_budget ? s->cfg.sample_budget_gb*1e9 : 20.0*(double)s->samp_cap, sp, need_rec);
+    if (!fixed_budget && (sp.mode != want_mode || need_rec > s->samp_cap)) {
         size_t free_b = 0, total_b = 0;
         HIP_OK(hipMemGetInfo(&free_b, &total_b));
         plan_splat((double)free_b + 20.0*(double)s->samp_cap - 16e9, sp, need_rec);
@@ -4326,8 +4393,7 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool prof_resolve = (g_profiling >> RT_KERNEL_RESOLVE) & 1u;
     if (prof_resolve) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
-    uint32_t tall_px = RES_TALL_PIXELS;
-    if (const char* e = getenv("RT_RES_TALL_PIXELS")) tall_px = (uint32_t)strtoul(e, nullptr, 0);   // tests: both heights
+    const uint64_t tall_px = s->cfg.resolve_tall_pixels > 0 ? (uint64_t)s->cfg.resolve_tall_pixels : RES_TALL_PIXELS;
     const bool tall = fp.pixels >= tall_px;
     const int rry = tall ? RT_RES_RY_TALL : RT_RES_RY;
     dim3 rgrid((w + RES_BX - 1) / RES_BX, (h + RES_BY*rry - 1) / (RES_BY*rry));

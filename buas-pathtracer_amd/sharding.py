@@ -32,7 +32,15 @@ def render_frame_sharded(render_shard, accum, rank, world, group=None, scratch=N
     buf = scratch if scratch is not None else accum.new_zeros(accum.shape)
     buf.zero_()
     stats = render_shard(rank, world, buf)
-    dist.reduce(buf, dst=0, group=group)
+    if buf.is_cuda and dist.get_backend(group) == "gloo":
+        # gloo reduces host tensors: stage the frame through host memory (the CPU-side test path;
+        # RCCL reduces the device buffer in place over xGMI)
+        host = buf.cpu()
+        dist.reduce(host, dst=0, group=group)
+        if rank == 0:
+            buf.copy_(host)
+    else:
+        dist.reduce(buf, dst=0, group=group)
     if rank == 0:
         accum.add_(buf)
     return stats

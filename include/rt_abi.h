@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---------------------------------------------------------------- status */
 enum rt_status {
@@ -406,6 +406,34 @@ int rt_set_env_sampling(int mode);
 /* discard_current_render (RT/raytracer.cpp:686-690): polled between wavefront
  * iterations; the render in flight returns RT_ERROR_CANCELLED. */
 int rt_cancel(rt_scene* scene);
+
+/* Per-scene configuration of the wavefront schedule and the splat (none of it changes a
+ * sample's bits; splat_mode and partitions change the float summation order of a pixel).
+ * Two scenes in one process may differ.  rt_scene_upload starts a scene from
+ * rt_scene_default_config(), then applies the test-override environment variables once
+ * (RT_SPLAT, RT_PARTITIONS, RT_FUSE_PATHS, RT_SPLAT_CHUNK, RT_SPLAT_RING,
+ * RT_SAMPLE_BUDGET_GB, RT_RES_TALL_PIXELS, RT_DEBUG_TRAVERSAL); nothing reads the
+ * environment per frame.  A field at RT_CONFIG_INHERIT follows the process-wide setter
+ * above at each frame (rt_set_splat_mode / rt_set_shard_mode / rt_set_env_sampling /
+ * rt_set_path_pool), so callers of those setters see no change. */
+#define RT_CONFIG_INHERIT (-1)
+typedef struct rt_scene_config {
+    int32_t  splat_mode;            /* rt_splat_mode, or RT_CONFIG_INHERIT                          */
+    int32_t  shard_mode;            /* rt_shard_mode, or RT_CONFIG_INHERIT                          */
+    int32_t  env_sampling;          /* 0 / 1, or RT_CONFIG_INHERIT                                  */
+    int32_t  partitions;            /* concurrent partitions (streams) per frame, 1..8; 0 = auto (4) */
+    int64_t  path_pool;             /* in-flight paths per partition; 0 = rt_set_path_pool / auto    */
+    int64_t  fuse_paths;            /* fused drain below this many live paths; -1 = auto, 0 = never */
+    int32_t  splat_chunk;           /* streaming splat: passes per resolve; 0 = auto                 */
+    int32_t  splat_ring;            /* streaming splat: record-ring passes per partition; 0 = auto   */
+    double   sample_budget_gb;      /* HBM for sample records; < 0 = auto (free HBM less 16 GB)      */
+    int64_t  resolve_tall_pixels;   /* exact splat: 8-row gather strips from this many pixels; 0 = auto */
+    int32_t  debug_traversal;       /* 1: longest-traversal diagnostics to stderr                   */
+    int32_t  reserved[7];
+} rt_scene_config;
+int rt_scene_default_config(rt_scene_config* out);
+int rt_scene_get_config(const rt_scene* scene, rt_scene_config* out);
+int rt_scene_set_config(rt_scene* scene, const rt_scene_config* config);
 
 #ifdef __cplusplus
 }

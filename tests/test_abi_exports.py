@@ -24,7 +24,7 @@ def test_every_declared_symbol_is_exported(rt):
     assert len(names) > 40
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.rt_abi_version() == 4
+    assert lib.rt_abi_version() == 5
 
 
 def test_ctypes_table_covers_header(rt):
@@ -48,3 +48,16 @@ def test_no_cpu_fallback_without_gpu(rt):
     with pytest.raises(rt.RenderError) as e:
         rt.DeviceScene(scene, 0)
     assert e.value.code == rt.abi.RT_ERROR_NO_DEVICE
+
+
+def test_scene_config_defaults(rt):
+    """rt_scene_default_config (no device needed): every per-scene setting starts at 'inherit the
+    process setter' or 'auto', and the ctypes mirror has the C layout."""
+    import ctypes as C
+    a = rt.abi
+    assert C.sizeof(a.SceneConfig) == 88
+    c = a.SceneConfig()
+    assert rt.lib().rt_scene_default_config(C.byref(c)) == 0
+    assert (c.splat_mode, c.shard_mode, c.env_sampling) == (a.RT_CONFIG_INHERIT,) * 3
+    assert (c.partitions, c.path_pool, c.fuse_paths, c.splat_chunk, c.splat_ring) == (0, 0, -1, 0, 0)
+    assert c.sample_budget_gb < 0 and c.resolve_tall_pixels == 0 and c.debug_traversal == 0

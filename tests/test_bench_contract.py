@@ -43,3 +43,12 @@ def test_step_stats_table(bench):
         e = sj[k]
         assert e["steps_per_ray"] >= e["interior_per_ray"] + e["leaf_per_ray"] > 0
         assert 0.0 < e["simd_efficiency"] <= 1.0
+
+
+def test_host_cores(bench):
+    """The CPU baseline's thread count is the cores this process may use: the affinity mask capped
+    by the cgroup CPU quota, never more than os.cpu_count()."""
+    hc = bench.host_cores()
+    assert 1 <= hc["cores"] <= hc["affinity"] <= hc["nproc"]
+    if hc["cgroup_quota_cores"] is not None:
+        assert hc["cores"] <= max(1, int(hc["cgroup_quota_cores"] + 0.5))

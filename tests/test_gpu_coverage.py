@@ -217,6 +217,13 @@ def test_pass_sharded_frames_sum(rt, n, mode):
                 ex, es = dev.render(cam, st, fc, 320, 200, shard_index=0, shard_count=n)
             finally:
                 rt.set_shard_mode(rt.abi.RT_SHARD_TILES)
+        # the last shard too: its passes start past 0, so a misplaced record would show here
+        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+            rt.set_shard_mode(rt.abi.RT_SHARD_PASSES)
+            try:
+                exl, esl = dev.render(cam, st, fc, 320, 200, shard_index=n - 1, shard_count=n)
+            finally:
+                rt.set_shard_mode(rt.abi.RT_SHARD_TILES)
     finally:
         dev.close()
     total = sum(p[0].astype(np.float64) for p in parts)
@@ -225,5 +232,66 @@ def test_pass_sharded_frames_sum(rt, n, mode):
     assert sum(p[1].closest_hit_rays for p in parts) == fs.closest_hit_rays
     assert sum(p[1].shadow_rays for p in parts) == fs.shadow_rays
     assert rel_l2(total, full) <= (1e-5 if mode == "stream" else 1e-4)
-    assert es.splat_mode == rt.abi.RT_SPLAT_STREAM
-    assert np.array_equal(ex, parts[0][0]) or mode == "atomic"
+    assert es.splat_mode == esl.splat_mode == rt.abi.RT_SPLAT_STREAM
+    assert (np.array_equal(ex, parts[0][0]) and np.array_equal(exl, parts[-1][0])) or mode == "atomic"
+
+
+@pytest.mark.parametrize("want", ["stream", "exact"])
+def test_pass_shards_wide_filter(rt, want):
+    """A filter radius past what k_resolve_tiles stages (kernel_size 16 > 12): a whole frame takes
+    the exact gather, a pass shard the atomic splat (its records would otherwise be placed at its
+    first pass in an array sized for its own passes).  Every shard of 3, the last one
+    included, sums with the others to the single-rank frame."""
+    scene, cam, st, fc, post = rt.load_preset("c1", 160, 128)
+    st.samples_per_pixel = 9
+    wide = rt.abi.FilterCache.from_buffer_copy(fc)
+    wide.kernel_size = 16                     # the Mitchell LUT stretched over a 16-pixel radius
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        m = rt.abi.RT_SPLAT_EXACT if want == "exact" else rt.abi.RT_SPLAT_STREAM
+        dev.configure(splat_mode=m)
+        full, fs = dev.render(cam, st, wide, 160, 128)
+        dev.configure(shard_mode=rt.abi.RT_SHARD_PASSES)
+        parts = [dev.render(cam, st, wide, 160, 128, shard_index=r, shard_count=3) for r in range(3)]
+    finally:
+        dev.close()
+    total = sum(p[0].astype(np.float64) for p in parts)
+    cpu, cs = ob.render(scene.desc(), cam, st, wide, 160, 128, rng_mode=0, threads=8)
+    REPORT[f"pass_shards_wide_filter_{want}"] = {"rel_l2_sum_vs_full": rel_l2(total, full), "rel_l2_full_vs_oracle": rel_l2(full, cpu),
+                                                 "modes": [int(fs.splat_mode)] + [int(p[1].splat_mode) for p in parts]}
+    assert fs.splat_mode == rt.abi.RT_SPLAT_EXACT
+    assert all(p[1].splat_mode == rt.abi.RT_SPLAT_ATOMIC for p in parts)
+    assert (fs.closest_hit_rays, fs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
+    assert sum(p[1].closest_hit_rays for p in parts) == fs.closest_hit_rays
+    assert rel_l2(full, cpu) <= 1e-6
+    assert rel_l2(total, full) <= 1e-4
+
+
+def test_scene_config_is_per_scene(rt, monkeypatch):
+    """rt_scene_config: two scenes in one process render with their own splat modes; the
+    environment is read once at upload (a variable set afterwards changes nothing); a bad
+    value is rejected with RT_ERROR_INVALID and leaves the configuration as it was."""
+    scene, cam, st, fc, post = rt.load_preset("c1", 128, 128)
+    st.samples_per_pixel = 4
+    a, b = rt.DeviceScene(scene, 0), None
+    try:
+        monkeypatch.setenv("RT_PARTITIONS", "1")
+        b = rt.DeviceScene(scene, 0)                     # uploaded with the override
+        monkeypatch.setenv("RT_SPLAT", "2")              # after both uploads: ignored
+        assert a.config().partitions == 0 and b.config().partitions == 1
+        a.configure(splat_mode=rt.abi.RT_SPLAT_EXACT)
+        fa, sa = a.render(cam, st, fc, 128, 128)
+        fb, sb = b.render(cam, st, fc, 128, 128)
+        assert sa.splat_mode == rt.abi.RT_SPLAT_EXACT and sb.splat_mode == rt.abi.RT_SPLAT_STREAM
+        assert (sa.closest_hit_rays, sa.shadow_rays) == (sb.closest_hit_rays, sb.shadow_rays)
+        assert rel_l2(fa, fb) <= 1e-5
+        before = a.config()
+        with pytest.raises(rt.RenderError):
+            a.configure(partitions=9)
+        with pytest.raises(rt.RenderError):
+            a.configure(splat_mode=7)
+        assert bytes(a.config()) == bytes(before)
+    finally:
+        a.close()
+        if b is not None:
+            b.close()

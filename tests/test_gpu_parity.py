@@ -191,8 +191,7 @@ def test_frame_bitwise_vs_reference_order(which, w, h, strip, request, monkeypat
     Both strip heights of k_resolve run: 4 rows, and the 8 rows whole-frame shards of
     >= 1.6M pixels use (forced here by RT_RES_TALL_PIXELS=1)."""
     rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
-    monkeypatch.setenv("RT_RES_TALL_PIXELS", "1" if strip == "8row" else "4294967295")
-    with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+    with dev.configured(resolve_tall_pixels=1 if strip == "8row" else 0xFFFFFFFF, splat_mode=rt.abi.RT_SPLAT_EXACT):
         gpu, gs = dev.render(cam, st, fc, w, h)
     assert gs.splat_mode == rt.abi.RT_SPLAT_EXACT
     cpu, _ = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1)
@@ -221,9 +220,9 @@ def test_stream_splat_vs_reference_order(which, w, h, request):
     assert np.isfinite(gpu).all() == np.isfinite(cpu).all()
 
 
-@pytest.mark.parametrize("env", [{"RT_SPLAT_CHUNK": "1", "RT_SPLAT_RING": "1"}, {"RT_SPLAT_CHUNK": "3", "RT_SPLAT_RING": "5"},
-                                 {"RT_SPLAT_CHUNK": "1000"}])
-def test_stream_splat_deterministic_in_chunking(c3small, env, monkeypatch):
+@pytest.mark.parametrize("env", [{"splat_chunk": 1, "splat_ring": 1}, {"splat_chunk": 3, "splat_ring": 5},
+                                 {"splat_chunk": 1000}])
+def test_stream_splat_deterministic_in_chunking(c3small, env):
     """k_resolve_tiles' result does not depend on how the passes are split between its
     launches or on the record ring's size (a one-pass ring throttles the sample claims):
     the frames are bit-identical to the default streaming frame, and to a second run."""
@@ -233,22 +232,21 @@ def test_stream_splat_deterministic_in_chunking(c3small, env, monkeypatch):
     ref, rs = dev.render(cam, st, fc, 192, 108)
     again, _ = dev.render(cam, st, fc, 192, 108)
     assert np.array_equal(ref, again)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    got, gs = dev.render(cam, st, fc, 192, 108)
+    with dev.configured(**env):
+        got, gs = dev.render(cam, st, fc, 192, 108)
     REPORT["stream_chunking_" + "_".join(f"{k}={v}" for k, v in env.items())] = {
         "frame_equal": bool(np.array_equal(ref, got)), "iterations": [int(rs.iterations), int(gs.iterations)]}
     assert (gs.closest_hit_rays, gs.shadow_rays) == (rs.closest_hit_rays, rs.shadow_rays)
     assert np.array_equal(ref, got)
 
 
-def test_stream_splat_box_filter_bit_exact(c1, monkeypatch):
+def test_stream_splat_box_filter_bit_exact(c1):
     """With one partition the streaming splat of the box filter adds each pixel's samples in
     sample order, the reference's order: bit-identical to the oracle's frame."""
     rt, scene, cam, st, fc, dev = c1
-    monkeypatch.setenv("RT_PARTITIONS", "1")
     box = rt.load_reconstruction_kernel("Box")
-    gpu, _ = dev.render(cam, st, box, 256, 256)
+    with dev.configured(partitions=1):
+        gpu, _ = dev.render(cam, st, box, 256, 256)
     cpu, _ = ob.render(scene.desc(), cam, st, box, 256, 256, rng_mode=0, threads=1)
     assert np.array_equal(gpu, cpu)
 
@@ -350,7 +348,7 @@ def test_atomic_splat_fallback(rt, monkeypatch, how):
     dev = rt.DeviceScene(scene, 0)
     try:
         if how == "budget":
-            monkeypatch.setenv("RT_SAMPLE_BUDGET_GB", "0")
+            dev.configure(sample_budget_gb=0.0)
             gpu, stats = dev.render(cam, st, fc, 128, 128)
         else:
             with rt.splat_mode(rt.abi.RT_SPLAT_ATOMIC):
@@ -377,7 +375,7 @@ def test_rcp_cr_exhaustive(rt):
 
 
 @pytest.mark.parametrize("which,w,h,spp", [("c3small", 192, 108, 24), ("c4small", 192, 108, 16), ("c1", 256, 256, 16)])
-def test_fused_drain_matches_separate_kernels(which, w, h, spp, request, monkeypatch):
+def test_fused_drain_matches_separate_kernels(which, w, h, spp, request):
     """The frame's drain fused into k_drain (each lane runs a path's remaining bounces) computes
     the same per-sample bits as the separate extend / shade / connect launches: frames (exact and
     streaming splat), per-sample radiance of the explicit-sample path and every ray count are
@@ -390,15 +388,12 @@ def test_fused_drain_matches_separate_kernels(which, w, h, spp, request, monkeyp
     xy = rng.integers(0, [w, h], size=(20000, 2)).astype(np.uint32)
     s = rng.integers(0, spp, size=20000).astype(np.uint32)
     out = {}
-    for name, val in (("off", "0"), ("default", None), ("all", "1000000000")):
-        if val is None:
-            monkeypatch.delenv("RT_FUSE_PATHS", raising=False)
-        else:
-            monkeypatch.setenv("RT_FUSE_PATHS", val)
-        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
-            ex, es = dev.render(cam, st, fc, w, h)
-        sm, ss = dev.render(cam, st, fc, w, h)
-        samp, ts = dev.trace_samples(cam, st, w, h, xy, s)
+    for name, val in (("off", 0), ("default", -1), ("all", 1000000000)):
+        with dev.configured(fuse_paths=val):
+            with dev.configured(splat_mode=rt.abi.RT_SPLAT_EXACT):
+                ex, es = dev.render(cam, st, fc, w, h)
+            sm, ss = dev.render(cam, st, fc, w, h)
+            samp, ts = dev.trace_samples(cam, st, w, h, xy, s)
         out[name] = (ex, sm, samp, [(int(x.closest_hit_rays), int(x.shadow_rays), int(x.traced_rays[0]),
                                      int(x.traced_rays[1])) for x in (es, ss, ts)], int(ss.iterations))
     ref = out["off"]
@@ -415,7 +410,7 @@ def test_fused_drain_matches_separate_kernels(which, w, h, spp, request, monkeyp
 
 
 @pytest.mark.parametrize("depth", [0, 1, 2])
-def test_fused_drain_shallow_paths(c1, depth, monkeypatch):
+def test_fused_drain_shallow_paths(c1, depth):
     """max_bounce_count 0 (nothing traced: every path finished at generation), 1 and 2: the fused
     drain gives the separate kernels' frame and ray counts, and the oracle's frame."""
     rt, scene, cam, st, fc, dev = c1
@@ -423,9 +418,8 @@ def test_fused_drain_shallow_paths(c1, depth, monkeypatch):
     st.max_bounce_count = depth
     st.samples_per_pixel = 8
     out = []
-    for val in ("0", "1000000000"):
-        monkeypatch.setenv("RT_FUSE_PATHS", val)
-        with rt.splat_mode(rt.abi.RT_SPLAT_EXACT):
+    for val in (0, 1000000000):
+        with dev.configured(fuse_paths=val, splat_mode=rt.abi.RT_SPLAT_EXACT):
             out.append(dev.render(cam, st, fc, 256, 256))
     cpu, cs = ob.render(scene.desc(), cam, st, fc, 256, 256, rng_mode=0, threads=1)
     (a, as_), (b, bs) = out
