@@ -397,32 +397,49 @@ bool parse_obj(char* input, std::vector<rt_v3>& tris, std::vector<rt_v3>& normal
 }
 
 // parse_hdr (RT/assets.cpp:423-618) + decode_radiance_color (:411-421)
+// match_word_ (:115-129): leading spaces (only ' ') skipped, then a prefix match
 bool match_word(char** s, const char* w) {
     char* at = *s;
-    while (*at == ' ' || *at == '\t') ++at;
+    while (*at == ' ') ++at;
     size_t n = strlen(w);
     if (strncmp(at, w, n) == 0) { *s = at + n; return true; }
     return false;
 }
+// parse_u32 (:147-160): strtoul with base 0 (its own whitespace skip; "010" is octal)
 bool parse_u32(char** s, uint32_t* out) {
-    char* at = *s;
-    while (*at == ' ' || *at == '\t') ++at;
     char* end;
-    unsigned long v = strtoul(at, &end, 10);
-    if (end == at) return false;
+    unsigned long v = strtoul(*s, &end, 0);
+    if (end == *s) return false;
     *out = (uint32_t)v; *s = end; return true;
+}
+bool parse_f32(char** s, float* out) {                 // :132-145
+    char* end;
+    float v = strtof(*s, &end);
+    if (end == *s) return false;
+    *out = v; *s = end; return true;
 }
 
 bool parse_hdr(const std::vector<char>& file, uint32_t* w_out, uint32_t* h_out, std::vector<rt_v3>& pixels) {
     char* at = const_cast<char*>(file.data());
     const char* file_end = file.data() + file.size() - 1;
     int x_adv = 1, y_adv = -1;
+    // the header (:446-492): up to the first empty line; FORMAT and PRIMARIES are read, a
+    // missing '=' after either is a malformed header, every other line is skipped.  The XYZ
+    // format and unknown formats are read as RGB (the reference warns and goes on).
     while (at < file_end && *at) {
         if (*at == '\n') { ++at; break; }
+        if (match_word(&at, "FORMAT")) {
+            if (!match_word(&at, "=")) { set_err("HDR PARSE ERROR: Malformed header."); return false; }
+            if (!match_word(&at, "32-bit_rle_rgbe")) (void)match_word(&at, "32-bit_rle_xyz");
+        } else if (match_word(&at, "PRIMARIES")) {
+            if (!match_word(&at, "=")) { set_err("HDR PARSE ERROR: Malformed header."); return false; }
+            float prim[8];                                 // parsed and unused, as in the reference
+            for (int i = 0; i < 8 && parse_f32(&at, &prim[i]); ++i) {}
+        }
         while (at < file_end && *at && *at != '\n') ++at;
         if (at < file_end && *at == '\n') ++at;
     }
-    if (at >= file_end) { set_err("HDR PARSE ERROR: Unexpected end of file while parsing header."); return false; }
+    if (at >= file_end || !*at) { set_err("HDR PARSE ERROR: Unexpected end of file while parsing header."); return false; }
     uint32_t w = 0, h = 0;
     if (match_word(&at, "+Y")) y_adv = 1; else if (match_word(&at, "-Y")) y_adv = -1;
     else { set_err("HDR PARSE ERROR: Failed to parse resolution string (+/-Y)."); return false; }
