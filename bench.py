@@ -204,8 +204,9 @@ def main():
     # Synthetic assets go through their files (the OBJ / RGBE parsers) on one rank only; ranks
     # started together build them in memory, so none can read another's file mid-write.
     asset_dir = None
-    if world == 1 and os.path.isdir(os.path.join(ROOT, "gpurun_out")):
-        asset_dir = os.path.join(ROOT, "gpurun_out", "assets")
+    if world == 1:
+        import tempfile
+        asset_dir = os.path.join(tempfile.gettempdir(), f"rt_assets_{os.getuid()}")
         os.makedirs(asset_dir, exist_ok=True)
     shard_mode = rt.abi.RT_SHARD_PASSES if args.shard_mode == "passes" else rt.abi.RT_SHARD_TILES
     stream = torch.cuda.current_stream(device)
@@ -241,10 +242,15 @@ def main():
     # marker that costs the other launches ~0.5 % of the frame (2.4 % for all stages).
     rt.lib().rt_set_profiling(1)
     wms = [0.0] * 6
+    wl = [0] * 6                    # warm-up launches per stage, and the rays the trace stages got
+    wtraced = [0, 0]
     for _ in range(args.warmup):
         s = step()
         for k in range(6):
             wms[k] += s.kernel_ms[k] / args.warmup
+            wl[k] += s.kernel_launches[k]
+        wtraced[0] += s.traced_rays[0]
+        wtraced[1] += s.traced_rays[1]
     torch.cuda.synchronize(device)
     if args.warmup:
         dom_stage = max(range(5), key=lambda k: wms[k])
@@ -339,8 +345,8 @@ def main():
         traffic = isolated = None
         try:
             with open(args.traffic_json) as f:
-                tj = json.load(f)
-            ent = tj.get("kernels", {}).get(KERNEL[dom]) if tj.get("config") == args.config else None
+                tj = json.load(f).get("configs", {}).get(args.config, {})
+            ent = tj.get("kernels", {}).get(KERNEL[dom])
             # measured on launches of the same size (units per launch within 10 %), else stale
             same = ent and (not ent.get("units_per_launch") or
                             abs(ent["units_per_launch"] / max(units_per_launch, 1.0) - 1.0) <= 0.1)
@@ -352,20 +358,30 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
         # Traversal kernels are bound by dependent L2 / Infinity Cache fetches, not HBM: their
-        # second figure is the bytes each step fetches (profiles/step_stats.json, from an
-        # RT_STEP_STATS build) over the same launch time, against the L2 gather rate
-        # (MI355X_MICROARCH.md, rows shared by every workgroup: 16.8-18.8 TB/s).
+        # second figure is the bytes the steps fetch (steps per ray from profiles/step_stats.json, an
+        # RT_STEP_STATS build, x 128 B) over the launches' HIP-event time in the warm-up frames (every
+        # stage timed there), against the L2 gather rate (MI355X_MICROARCH.md, rows shared by every
+        # workgroup: 16.8-18.8 TB/s).  Reported for both trace kernels whichever kernel dominates.
         traversal = None
         try:
             with open(os.path.join(ROOT, "profiles", "step_stats.json")) as f:
                 sj = json.load(f)
-            ent = sj.get(KERNEL[dom]) if sj.get("config") == args.config else None
-            if ent and mean_launch_s > 0:
-                tb = ent["steps_per_ray"] * sj["bytes_per_step"] * units_per_launch
-                t_gbs = tb / mean_launch_s / 1e9
-                traversal = {"bytes_per_ray": round(ent["steps_per_ray"] * sj["bytes_per_step"], 1),
-                             "bytes_per_launch": round(tb), "achieved": round(t_gbs, 1), "peak": L2_PEAK_GBS,
-                             "unit": "GB/s", "frac": round(t_gbs / L2_PEAK_GBS, 4), "source": sj.get("source")}
+            per_cfg = sj.get("configs", {}).get(args.config)
+            if per_cfg and args.warmup:
+                traversal = {"peak": L2_PEAK_GBS, "unit": "GB/s", "source": sj.get("source"),
+                             "timing": "warm-up frames, HIP events on each partition's stream (shared GPU)"}
+                for stage, kname, rays in (("extend", "k_extend", wtraced[0]), ("connect", "k_connect", wtraced[1])):
+                    ent = per_cfg.get(kname)
+                    k = STAGES.index(stage)
+                    if not ent or not wl[k] or wms[k] <= 0:
+                        continue
+                    per_launch = rays / wl[k]
+                    tb = ent["steps_per_ray"] * sj["bytes_per_step"] * per_launch
+                    mean_s = wms[k] * args.warmup / wl[k] / 1e3
+                    t_gbs = tb / mean_s / 1e9
+                    traversal[kname] = {"rays_per_launch": round(per_launch), "steps_per_ray": ent["steps_per_ray"],
+                                        "bytes_per_launch": round(tb), "mean_launch_ms": round(mean_s * 1e3, 4),
+                                        "achieved": round(t_gbs, 1), "frac": round(t_gbs / L2_PEAK_GBS, 4)}
         except (OSError, ValueError, KeyError):
             pass
         ref = wms if args.warmup else [x / args.steps for x in kms]        # all stages: warm-up frames

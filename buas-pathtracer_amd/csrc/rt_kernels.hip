@@ -1160,7 +1160,7 @@ struct PathOut {
 };
 struct Pool {
     uint32_t n;
-    float4* ray_o;       // o.xyz | w: pixel index bits
+    float4* ray_o;       // o.xyz | w: the pixel, x | y << 16 (frames are at most 65535 a side)
     float4* ray_d;       // d.xyz | w: sample offset bits
     float4* thr;         // throughput.xyz | w: vignette
     float4* L;           // total_color.xyz | w: flags bits (bounce 0-7, specular 8, stack_at 9-15)
@@ -1249,6 +1249,9 @@ struct Counters {
 struct FrameParams {
     uint32_t w, h, frame_count, total_frame_index;
     uint32_t tile_w, tile_h, tcx;
+    // ceil(2^32 / tile_w), ceil(2^32 / tile_h), ceil(2^64 / pixels) (set_divisors): a coordinate's tile and a
+    // sample number's pass by a multiply-high instead of the integer division expansion (div16, div_pixels)
+    uint64_t tw_m, th_m, px_m;
     uint32_t pixels;                // P: pixels owned by this shard
     uint32_t ntiles;
     const uint32_t* tile_ids;       // owned tiles
@@ -1433,6 +1436,14 @@ RT_D void apply_lens_distortion(float amount, uint32_t w, uint32_t h, float& u, 
 
 RT_D uint32_t pack_flags(uint32_t bounce, uint32_t spec, uint32_t at) { return bounce | (spec << 8) | (at << 9); }
 
+// x / d for x, d < 2^16 with m = ceil(2^32 / d): floor(x*m / 2^32) = floor(x / d + e) with
+// 0 <= e < x / 2^32 < 1 / d, which cannot reach the next integer (Granlund & Montgomery 1994).
+RT_D uint32_t div16(uint32_t x, uint64_t m) { return (uint32_t)(((uint64_t)x*m) >> 32); }
+// k / P for k < 2^32, P < 2^32 with m = ceil(2^64 / P): the same bound with 2^64
+RT_D uint32_t div_pixels(uint32_t k, uint64_t m) { return (uint32_t)__umul64hi((uint64_t)k, m); }
+// a pixel's tile (RT/raytracer.cpp:551-560 numbering: row-major over tcx tiles per row)
+RT_D uint32_t tile_of(const FrameParams& fp, uint32_t x, uint32_t y) { return div16(y, fp.th_m)*fp.tcx + div16(x, fp.tw_m); }
+
 // ======================================================================
 // Kernels
 // ======================================================================
@@ -1517,7 +1528,7 @@ __global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out
 RT_D V2 sample_jitter(const DevScene& sc, const rt_settings& st, const FrameParams& fp, uint32_t x, uint32_t y,
                       uint32_t s) {
     const uint32_t canonical = fp.frame_count + s;
-    const uint32_t tile = (y / fp.tile_h)*fp.tcx + (x / fp.tile_w);
+    const uint32_t tile = tile_of(fp, x, y);
     Rng rng = random_seed(sample_seed(fp.total_frame_index, fp.frame_count, tile, y*fp.w + x, canonical));
     const SamplerState ss = {x, y, canonical, st.sampling_strategy};
     const V2 aa = sample_2d(sc, ss, rng, S_AA, 0);
@@ -1545,7 +1556,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         const uint2 fk = ldnt(&pool.fin_k[slot]);
         const uint32_t pixel = ldnt(&pool.fin_px[slot]);
         const uint32_t s = fp.list_xy ? fp.list_s[fk.x] : fk.x;
-        const V2 j = sample_jitter(sc_g, st, fp, pixel % fp.w, pixel / fp.w, s);
+        const V2 j = sample_jitter(sc_g, st, fp, pixel & 0xFFFFu, pixel >> 16, s);
         splat_sample(fp, pool, ld3(fl), fl.w, make_float2(j.x, j.y), fk.x, fk.y);
     }
     // Each wave's survivors fill its first slots; the rest take new paths, claiming consecutive
@@ -1578,8 +1589,8 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
             x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
         } else {
             uint32_t pass;
-            if (k < 0x100000000ull) {                        // 32-bit division when it suffices
-                pass = (uint32_t)k / fp.pixels;
+            if (k < 0x100000000ull && fp.px_m) {             // a multiply-high when k fits 32 bits
+                pass = div_pixels((uint32_t)k, fp.px_m);
                 p = (uint32_t)k - pass*fp.pixels;
             } else {
                 pass = (uint32_t)(k / fp.pixels);
@@ -1589,7 +1600,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
             x = xy & 0xFFFFu; y = xy >> 16; s = pass;
         }
         uint32_t canonical = fp.frame_count + s;
-        uint32_t tile = (y / fp.tile_h)*fp.tcx + (x / fp.tile_w);
+        uint32_t tile = tile_of(fp, x, y);
         Rng rng = random_seed(sample_seed(fp.total_frame_index, fp.frame_count, tile, y*fp.w + x, canonical));
         // camera (RT/raytracer.cpp:381-401)
         float hfw = fp.half_film_w*fp.focus_distance;
@@ -1616,7 +1627,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         vig = vig*vig*vig*vig;
         vig = lerpf_(1.0f, vig, st.vignette_strength);
         nro = jcp; nrd = rd;
-        pool.ray_o[slot] = make_float4(jcp.x, jcp.y, jcp.z, __uint_as_float(y*fp.w + x));
+        pool.ray_o[slot] = make_float4(jcp.x, jcp.y, jcp.z, __uint_as_float(x | (y << 16)));
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
         pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
         cast = st.max_bounce_count > 0;
@@ -2088,7 +2099,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         int32_t at = (int32_t)((flags >> 9) & 0x7Fu);
         uint32_t pixel = __float_as_uint(o4.w);
         uint32_t sample_off = __float_as_uint(d4.w);
-        uint32_t px = pixel % fp.w, py = pixel / fp.w;
+        uint32_t px = pixel & 0xFFFFu, py = pixel >> 16;            // no integer division
         uint32_t canonical = fp.frame_count + (fp.list_xy ? fp.list_s[sample_off] : sample_off);
         SamplerState ss = {px, py, canonical, st.sampling_strategy};
         Hit h;
@@ -2339,7 +2350,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
         uint32_t sh_light = 0;
         if (active) {
             const uint32_t canonical = fp.frame_count + (fp.list_xy ? fp.list_s[key] : key);
-            const SamplerState ss = {pixel % fp.w, pixel / fp.w, canonical, st.sampling_strategy};
+            const SamplerState ss = {pixel & 0xFFFFu, pixel >> 16, canonical, st.sampling_strategy};
 #if RT_SHADE_PROF
             unsigned long long prof[SP_N] = {};
 #endif
@@ -2366,7 +2377,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
         n_shadow += cast_shadow ? 1u : 0u;
         if (active && done) {
             const uint32_t s = fp.list_xy ? fp.list_s[key] : key;
-            const V2 j = sample_jitter(sc, st, fp, pixel % fp.w, pixel / fp.w, s);
+            const V2 j = sample_jitter(sc, st, fp, pixel & 0xFFFFu, pixel >> 16, s);
             splat_sample(fp, pool, total, vig, make_float2(j.x, j.y), key, p);
             active = false;
         } else if (active) {
@@ -3612,6 +3623,15 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     return RT_OK;
 }
 
+// FrameParams' multiply-high divisors (div16, div_pixels); tile sides and pixels are non-zero
+void set_divisors(FrameParams& fp) {
+    fp.tw_m = ((1ull << 32) + fp.tile_w - 1) / fp.tile_w;
+    fp.th_m = ((1ull << 32) + fp.tile_h - 1) / fp.tile_h;
+    // ceil(2^64 / P) = floor((2^64 - 1) / P) + 1 for P > 1; 2^64 does not fit, so P <= 1 keeps m = 0 and
+    // k_generate divides
+    fp.px_m = fp.pixels > 1 ? (~0ull / fp.pixels) + 1ull : 0ull;
+}
+
 void fill_camera(FrameParams& fp, const rt_camera* c) {
     fp.cp = rv3(c->p); fp.cx = rv3(c->x); fp.cy = rv3(c->y); fp.cz = rv3(c->z);
     fp.focus_distance = c->focus_distance;
@@ -4236,6 +4256,7 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         L.valid = true;
     }
     fp.pix_xy = s->d_pixmap;
+    set_divisors(fp);
     fill_camera(fp, camera);
     fp.lut = s->d_lut;
     fp.kernel_size = (int32_t)filter->kernel_size;
@@ -4351,6 +4372,26 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
                                 any = L.base[(size_t)ty*fp.tcx + tx] >= 0;
                         if (any) blocks.push_back(bx | (by << 16));
                     }
+                // XCD-aware order.  Blocks are dealt round robin over the 8 XCDs (b and b + 8 share one, each
+                // with its own L2: MI355X_MICROARCH.md), so the list gives each XCD one contiguous run of the
+                // blocks in column-major order: an XCD resolves its blocks top to bottom, and the filter-radius
+                // rows a block stages above its own were read into that L2 by the block before it.  The sums
+                // do not depend on the order (each pixel belongs to one block).
+                {
+                    std::vector<uint32_t> colmajor(blocks);
+                    std::stable_sort(colmajor.begin(), colmajor.end(), [](uint32_t a, uint32_t b) {
+                        return (a & 0xFFFFu) != (b & 0xFFFFu) ? (a & 0xFFFFu) < (b & 0xFFFFu) : (a >> 16) < (b >> 16);
+                    });
+                    // run x holds column-major positions [n*x/8, n*(x+1)/8); its k-th block goes to list
+                    // position 8k + x (in the last round, when the runs differ by one, in order)
+                    const size_t n = colmajor.size();
+                    std::vector<size_t> start(NSHARD + 1);
+                    for (int x = 0; x <= NSHARD; ++x) start[x] = n*(size_t)x / NSHARD;
+                    blocks.clear();
+                    for (size_t k = 0; blocks.size() < n; ++k)
+                        for (int x = 0; x < NSHARD; ++x)
+                            if (start[x] + k < start[x + 1]) blocks.push_back(colmajor[start[x] + k]);
+                }
                 const size_t aux = blocks.size() + 2*MAX_PARTITIONS;       // the pointer table, then the blocks
                 if (s->aux_cap < aux) {
                     if (s->d_aux) (void)hipFree(s->d_aux);
@@ -4478,6 +4519,7 @@ int rt_trace_samples(rt_scene* s, const rt_camera* camera, const rt_settings* st
     if (err) return err;
     if (!s || !camera || !pixel_xy || !sample_offset || !out || !w || !h || !tile_w || !tile_h) { set_error("null argument"); return RT_ERROR_INVALID; }
     if (!count) return RT_OK;
+    if (w > 65535 || h > 65535) { set_error("frame larger than 65535 pixels a side"); return RT_ERROR_INVALID; }
     for (uint32_t i = 0; i < count; ++i)
         if (pixel_xy[2*i] >= w || pixel_xy[2*i + 1] >= h) { set_error("sample pixel out of range"); return RT_ERROR_INVALID; }
     HIP_OK(hipSetDevice(s->device));
@@ -4491,6 +4533,7 @@ int rt_trace_samples(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.w = w; fp.h = h; fp.frame_count = frame_count; fp.total_frame_index = total_frame_index;
     fp.tile_w = tile_w; fp.tile_h = tile_h; fp.tcx = (w + tile_w - 1) / tile_w;
     fp.list_xy = d_xy; fp.list_s = d_s; fp.list_out = d_out;
+    set_divisors(fp);
     fill_camera(fp, camera);
     err = run_frame(s, st, fp, count, nullptr, SplatCfg{}, stats);
     if (!err && hipMemcpy(out, d_out, 20*(size_t)count, hipMemcpyDeviceToHost) != hipSuccess) { set_error("copy out"); err = RT_ERROR_DEVICE; }

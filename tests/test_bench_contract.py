@@ -28,8 +28,7 @@ def test_stage_tables_agree(bench):
 
 
 def test_traffic_table(bench):
-    tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))
-    assert tj["config"] == "c3"
+    tj = json.load(open(os.path.join(ROOT, "profiles", "traffic.json")))["configs"]["c3"]
     for stage in ("generate", "extend", "shade", "connect"):
         ent = tj["kernels"][bench.KERNEL[stage]]
         assert ent["hbm_bytes_per_launch"] > 0 and ent["isolated_mean_us"] > 0
@@ -38,11 +37,12 @@ def test_traffic_table(bench):
 
 def test_step_stats_table(bench):
     sj = json.load(open(os.path.join(ROOT, "profiles", "step_stats.json")))
-    assert sj["config"] == "c3" and sj["bytes_per_step"] == 128
-    for k in ("k_extend", "k_connect"):
-        e = sj[k]
-        assert e["steps_per_ray"] >= e["interior_per_ray"] + e["leaf_per_ray"] > 0
-        assert 0.0 < e["simd_efficiency"] <= 1.0
+    assert sj["bytes_per_step"] == 128 and {"c3", "c4"} <= set(sj["configs"])
+    for cfg in sj["configs"].values():
+        for k in ("k_extend", "k_connect"):
+            e = cfg[k]
+            assert e["steps_per_ray"] >= e["interior_per_ray"] + e["leaf_per_ray"] > 0
+            assert 0.0 < e["simd_efficiency"] <= 1.0
 
 
 def test_host_cores(bench):

@@ -2,7 +2,10 @@
 """Summarise rocprofv3 --pmc passes (tools/gpu_pmc.sh output) per kernel.
 
 usage: tools/pmc_summary.py gpurun_out/<TAG> [--out profiles/<name>.md] [--traffic profiles/traffic.json
-                            --bench-log gpurun_out/<TAG>/pass1.log]
+                            --config c3 --bench-log gpurun_out/<TAG>/pass1.log]
+
+--traffic merges this run's per-kernel bytes and isolated durations into the file's "configs"[<config>]
+entry (the other configurations' entries are kept), which bench.py reads for the `isolated` figures.
 
 Counter values are summed over every dispatch of a kernel; SQ counters on gfx950 are
 summed over the shader engines.  FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM
@@ -50,6 +53,7 @@ def main():
     ap.add_argument("--out")
     ap.add_argument("--traffic")
     ap.add_argument("--bench-log")
+    ap.add_argument("--config", default="c3")
     a = ap.parse_args()
     val, disp, dur = load(a.tag_dir)
     lines = [f"# PMC summary: {a.tag_dir}", "",
@@ -108,7 +112,7 @@ def main():
         open(a.out, "w").write(text)
         json.dump(out, open(os.path.splitext(a.out)[0] + ".json", "w"), indent=1)
     if a.traffic and out:
-        rec = {"config": "c3", "source": a.tag_dir,
+        rec = {"source": a.tag_dir,
                "note": "HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (rocprofv3 --pmc, kernels serialized), "
                        "plus the serialized mean launch duration",
                "kernels": {KEYS.get(k, k): {"hbm_bytes_per_launch": (e["hbm_read_mb_per_launch"] + e["hbm_write_mb_per_launch"]) * 1e6,
@@ -124,8 +128,17 @@ def main():
                     rf = b.get("roofline") or {}
                     if rf.get("kernel") in rec["kernels"]:
                         rec["kernels"][rf["kernel"]]["units_per_launch"] = rf.get("units_per_launch")
-        json.dump(rec, open(a.traffic, "w"), indent=1)
-        print("wrote", a.traffic)
+        try:
+            allrec = json.load(open(a.traffic))
+        except (OSError, ValueError):
+            allrec = {}
+        if "configs" not in allrec:
+            allrec = {"note": "per configuration: HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE and the serialized "
+                              "mean launch duration (rocprofv3 --pmc, kernels serialized); tools/pmc_summary.py --traffic",
+                      "configs": {}}
+        allrec["configs"][a.config] = rec
+        json.dump(allrec, open(a.traffic, "w"), indent=1)
+        print("wrote", a.traffic, "configs", sorted(allrec["configs"]))
 
 
 if __name__ == "__main__":
