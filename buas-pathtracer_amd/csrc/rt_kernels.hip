@@ -1174,9 +1174,15 @@ struct Pool {
     uint16_t* mstack;    // [64][n]
     uint8_t*  state;     // S_FREE / S_TRACE / S_DONE per slot
     float4*   ext_rec[2];// extension queues (ping-pong), REC_Q float4 per ray: {o, slot}, {d, t after planes}, {1/d, -}
-    uint32_t* sh_slot;
-    float4*   sh_rec;    // shadow queue, REC_Q float4 per ray: {o, light id}, {d, max_t}, {1/d, -}
+    // The shadow queue.  RT_SH_STAGE (default): k_shade writes a queued shadow ray's record and
+    // contribution at its own slot as soon as the ray's prologue is done (so they are not held in
+    // registers across the next bounce's prologue), the queue entry is just that slot, and the
+    // NEE term's destination goes to sh_dst[slot] at the tail.  Otherwise all of it is at the queue
+    // position and sh_slot holds the destination.
+    uint32_t* sh_slot;   // [Q] RT_SH_STAGE: the slot holding the ray; else its destination
+    float4*   sh_rec;    // REC_Q float4 per ray: {o, light id}, {d, max_t}, {1/d, mesh list}
     float4*   sh_c;      // contribution.xyz
+    uint32_t* sh_dst;    // [N] RT_SH_STAGE: the NEE term's destination (survivor's nx slot or SH_FIN | entry)
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
     uint32_t* free_n;    // [blocks]: the block's slots past its survivors, for the next k_generate (k_shade)
     uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
@@ -1204,6 +1210,17 @@ struct Pool {
 // appends to come out as runs of consecutive slots (one run per wavefront).
 enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2 };
 constexpr int REC_Q = 3;     // float4 per queued ray record
+#ifndef RT_SH_STAGE
+#define RT_SH_STAGE 1
+#endif
+// k_shade writes a survivor's state before the ray prologues, total_color and the hit record after
+#ifndef RT_SHADE_EARLY
+#define RT_SHADE_EARLY 1
+#endif
+// k_shade keeps the values it only writes out at the end in LDS (needs RT_SHADE_EARLY)
+#ifndef RT_SHADE_STASH
+#define RT_SHADE_STASH RT_SHADE_EARLY
+#endif
 constexpr uint32_t SH_FIN = 0x80000000u;   // Pool::sh_slot: the shadow ray's path is in the finished array
 
 // Queues and fetch heads are sharded NSHARD ways (shard = blockIdx % NSHARD, the
@@ -1731,7 +1748,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 #endif
         if (OCC) {
             if (!tr.occluded) {
-                const uint32_t slot = pool.sh_slot[item];
+                const uint32_t slot = RT_SH_STAGE ? pool.sh_dst[item] : pool.sh_slot[item];
                 const float4 c = ldnt(&pool.sh_c[item]);
                 float4* const dst = (slot & SH_FIN) ? &pool.fin_L[slot & ~SH_FIN] : &pool.nx.L[slot];
                 float4 L = ldnt(dst);
@@ -1774,6 +1791,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
             if (!active && rank < avail) {
                 item = chunk_next + rank;
+                if (OCC && RT_SH_STAGE) item = pool.sh_slot[item];   // the k_shade slot that staged the ray
                 const float4* q = (OCC ? pool.sh_rec : pool.ext_rec[cur]) + REC_Q*(size_t)item;
                 const float4 o = ldnt(&q[0]), d = ldnt(&q[1]), iv = ldnt(&q[2]);
                 if (!OCC) item = __float_as_uint(o.w);            // the path's slot
@@ -1805,6 +1823,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 #define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(1, RT_SHADE_MAX_WAVES)))
 #elif defined(RT_SHADE_WAVES)
 #define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WAVES)))
+#elif RT_SHADE_STASH
+// 8 waves per SIMD (64 VGPRs) for the default instantiation (scene in LDS, no environment NEE),
+// which fits them without spills; the others need 66-67 and keep 7
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((IN_LDS && !ENV) ? 8 : 7)))
 #else
 #define RT_SHADE_ATTR
 #endif
@@ -2088,6 +2110,23 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     // that end here
     const bool made_fin = slot < pool.n && state0 == S_DONE;
     const unsigned long long made_fin_mask = __ballot(made_fin);
+#if RT_SHADE_STASH
+    // pixel, sample key, vignette and tile-list pixel: written out only at the end, so they wait in
+    // LDS (the thread's own entry, no barrier) instead of registers across the bounce and prologues
+    __shared__ uint4 stash[BLOCK];
+    if (valid || made_fin)
+        stash[threadIdx.x] = make_uint4(__float_as_uint(o4.w), __float_as_uint(d4.w), __float_as_uint(t4.w),
+                                        __float_as_uint(pn2.y));
+#define SH_META_PIXEL(m) __uint_as_float((m).x)
+#define SH_META_KEY(m) __uint_as_float((m).y)
+#define SH_META_VIG(m) __uint_as_float((m).z)
+#define SH_META_P(m) __uint_as_float((m).w)
+#else
+#define SH_META_PIXEL(m) o4.w
+#define SH_META_KEY(m) d4.w
+#define SH_META_VIG(m) t4.w
+#define SH_META_P(m) pn2.y
+#endif
     if (valid) {
         SP_MARK(t_load);
         Rng rng = {r4.x, r4.y, r4.z, r4.w};
@@ -2107,6 +2146,39 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         SP_ADD(SP_LOAD, t_load);
         done = shade_bounce<ENV>(sc, st, ss, pool, slot, h, ro, rd, thr, total, prev_pdf, bounce, is_spec, at, rng,
                                  cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light SP_PASS);
+#if RT_SHADE_EARLY
+        // The survivor's state that the two prologues below do not change goes out now, so the
+        // throughput, RNG and flags are not held in registers across them (total_color and the
+        // hit record follow the prologues).
+        cont = !done;
+#if RT_SHADE_STASH
+        const uint4 meta = stash[threadIdx.x];
+#else
+        const uint4 meta = {};
+#endif
+        {
+            const unsigned long long smask = __ballot(cont);
+            nslot = (slot & ~63u) + (uint32_t)__popcll(smask & ((1ull << __lane_id()) - 1ull));
+        }
+        if (cont) {
+            stnt(&pool.nx.ray_o[nslot], make_float4(ro.x, ro.y, ro.z, SH_META_PIXEL(meta)));
+            stnt(&pool.nx.ray_d[nslot], make_float4(rd.x, rd.y, rd.z, SH_META_KEY(meta)));
+            stnt(&pool.nx.thr[nslot], make_float4(thr.x, thr.y, thr.z, SH_META_VIG(meta)));
+            stnt(&pool.nx.prev_n[nslot], make_float2(prev_pdf, SH_META_P(meta)));
+            stnt(&pool.nx.rng[nslot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
+            pool.nx.state[nslot] = S_TRACE;
+            for (int32_t lv = 1; lv <= at; ++lv)
+                pool.nx.mstack[(size_t)lv*pool.n + nslot] = pool.mstack[(size_t)lv*pool.n + slot];
+        }
+        const unsigned long long fm = made_fin_mask | __ballot(done);
+        if (done) {                                        // everything but total_color
+            const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
+            stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(SH_META_KEY(meta)), __float_as_uint(SH_META_P(meta))));
+            stnt(&pool.fin_px[fidx], __float_as_uint(SH_META_PIXEL(meta)));
+        }
+        const float vig = SH_META_VIG(meta);
+        const uint32_t nflags = pack_flags(bounce, is_spec, (uint32_t)at);
+#endif
         if (cast_shadow) {
             // intersect_shadow_ray (:756): planes and the top level here; only rays that meet
             // a mesh are queued for k_trace<true>.  Nothing else adds to total_color after the
@@ -2115,8 +2187,34 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
             shadow = !spro.occluded && spro.bvh;
             if (!spro.occluded && !spro.bvh) total = add(total, sh_c);
+#if RT_SH_STAGE
+            if (shadow) {                                  // staged at the slot (Pool::sh_rec)
+                float4* q = pool.sh_rec + REC_Q*(size_t)slot;
+                stnt(&q[0], make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light)));
+                stnt(&q[1], make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t));
+                stnt(&q[2], make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist)));
+                stnt(&pool.sh_c[slot], make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f));
+            }
+#endif
             SP_ADD(SP_SHPRO, t_shpro);
         }
+#if RT_SHADE_EARLY
+        SP_MARK(t_store);
+        if (cont) stnt(&pool.nx.L[nslot], make_float4(total.x, total.y, total.z, __uint_as_float(nflags)));
+        if (done) {
+            const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
+            stnt(&pool.fin_L[fidx], make_float4(total.x, total.y, total.z, vig));
+        }
+        SP_ADD(SP_STORE, t_store);
+        nro = ro; nrd = rd;
+        if (cont) {                                        // next bounce's intersect_scene: planes + top level here
+            SP_MARK(t_cpro);
+            cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
+            enq = cpro.bvh;
+            stnt(&pool.nx.hit[nslot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
+            SP_ADD(SP_CPRO, t_cpro);
+        }
+#else
         cont = !done;
         nro = ro; nrd = rd;
         if (cont) {                                        // next bounce's intersect_scene: planes + top level here
@@ -2153,6 +2251,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                 pool.nx.mstack[(size_t)lv*pool.n + nslot] = pool.mstack[(size_t)lv*pool.n + slot];
         }
         SP_ADD(SP_STORE, t_store);
+#endif
     }
     SP_MARK(t_tail);
     const int nxt = cur ^ 1;
@@ -2164,9 +2263,14 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const unsigned long long fmask = __ballot(fin);
     const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fmask & ((1ull << __lane_id()) - 1ull));
     if (made_fin) {                                 // L = 0 with the vignette in .w (k_generate)
+#if RT_SHADE_STASH
+        const uint4 fmeta = stash[threadIdx.x];
+#else
+        const uint4 fmeta = {};
+#endif
         stnt(&pool.fin_L[fidx], pool.L[slot]);
-        stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(d4.w), __float_as_uint(pn2.y)));
-        stnt(&pool.fin_px[fidx], __float_as_uint(o4.w));
+        stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(SH_META_KEY(fmeta)), __float_as_uint(SH_META_P(fmeta))));
+        stnt(&pool.fin_px[fidx], __float_as_uint(SH_META_PIXEL(fmeta)));
     }
     const unsigned long long cmask = __ballot(cont);
     if (__lane_id() == 0) {
@@ -2189,12 +2293,17 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const uint32_t spos = shard*pool.shard_cap + tpos[1];
     if (shadow) {
         // the NEE term goes to the survivor's L in pool.nx, or to the finished entry
+#if RT_SH_STAGE
+        pool.sh_slot[spos] = slot;
+        pool.sh_dst[slot] = cont ? nslot : (SH_FIN | fidx);
+#else
         pool.sh_slot[spos] = cont ? nslot : (SH_FIN | fidx);
         float4* q = pool.sh_rec + REC_Q*(size_t)spos;
         stnt(&q[0], make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light)));
         stnt(&q[1], make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t));
         stnt(&q[2], make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist)));
         stnt(&pool.sh_c[spos], make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f));
+#endif
     }
     if (threadIdx.x == 0) pool.free_n[blockIdx.x] = ttot[5];
 #if RT_SHADE_PROF
@@ -3222,8 +3331,9 @@ int ensure_pool(Partition& pt, uint32_t n) {
     e |= alloc((void**)&p.ext_rec[1], 16*REC_Q*Q);
     e |= alloc((void**)&p.state, N);
     e |= alloc((void**)&p.sh_slot, 4*Q);
-    e |= alloc((void**)&p.sh_rec, 16*REC_Q*Q);
-    e |= alloc((void**)&p.sh_c, 16*Q);
+    e |= alloc((void**)&p.sh_rec, 16*REC_Q*(RT_SH_STAGE ? N : Q));
+    e |= alloc((void**)&p.sh_c, 16*(RT_SH_STAGE ? N : Q));
+    if (RT_SH_STAGE) e |= alloc((void**)&p.sh_dst, 4*N);
     if (e) { free_pool(pt); return RT_ERROR_OUT_OF_MEMORY; }
     p.n = n;
     return RT_OK;
