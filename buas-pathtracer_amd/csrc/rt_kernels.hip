@@ -810,7 +810,8 @@ struct Traversal {
             inv.e[1][0] = F[1].x; inv.e[1][1] = F[1].y; inv.e[1][2] = F[1].z; inv.e[1][3] = F[1].w;
             inv.e[2][0] = F[2].x; inv.e[2][1] = F[2].y; inv.e[2][2] = F[2].z; inv.e[2][3] = F[2].w;
             const Ray ir = make_ray(xform(inv, wo, 1.0f), xform(inv, wd, 0.0f), 0.0f);   // transform_ray :403-409
-            if (type == RT_PRIMITIVE_MESH) {                      // intersect_mesh :243-401
+            // LST: the prologue lists mesh instances only (spheres and boxes were tested there)
+            if (LST || type == RT_PRIMITIVE_MESH) {               // intersect_mesh :243-401
                 co = ir.o; cd = ir.d; cinv = ir.inv_d;
                 cflags = ir.neg | (ir.zero << 3) | ((sc.finite_boxes && finite_box_ray(ir.o, ir.inv_d)) ? 64u : 0u);
                 inst = pi; node_off = __float_as_uint(F[3].z); tri_off = __float_as_uint(F[3].w);
@@ -821,12 +822,14 @@ struct Traversal {
                 mode = TM_MESH;
                 return true;
             }
-            bool hit = false;
-            if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, F[3].z, t);
-            else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {F[3].z, F[3].w, F[4].x}, t);
-            if (hit) {
-                if (OCC) { occluded = true; mode = TM_DONE; return false; }
-                code = pi;
+            if (!LST) {
+                bool hit = false;
+                if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, F[3].z, t);
+                else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {F[3].z, F[3].w, F[4].x}, t);
+                if (hit) {
+                    if (OCC) { occluded = true; mode = TM_DONE; return false; }
+                    code = pi;
+                }
             }
             return true;
         }
@@ -1708,7 +1711,9 @@ constexpr int STEPS_PER_REFILL_SHADOW = RT_STEPS_PER_REFILL_SHADOW;
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
-template <bool OCC, bool LST>
+// DIAG (rt_scene_config::debug_traversal): count each query's steps for the longest-traversal report
+// (a separate instantiation: the counter is one more VGPR for the whole kernel)
+template <bool OCC, bool LST, bool DIAG>
 __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag,
                                                               int fuse) {
     if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
@@ -1735,7 +1740,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     uint32_t steps = 0;
     Traversal<OCC, LST> tr;
     auto finish = [&]() {
-        if (diag) {                                   // RT_DEBUG_TRAVERSAL: longest traversals
+        if (DIAG) {                                   // RT_DEBUG_TRAVERSAL: longest traversals
             atomicMax(&cnt->max_steps[OCC ? 1 : 0], steps);
             if (steps > 20000u) {
                 float* w = cnt->worst_ray[OCC ? 1 : 0];
@@ -1796,7 +1801,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                 const float4 o = ldnt(&q[0]), d = ldnt(&q[1]), iv = ldnt(&q[2]);
                 if (!OCC) item = __float_as_uint(o.w);            // the path's slot
                 tr.init_rec(sc, st, ld3(o), ld3(d), ld3(iv), d.w, OCC ? __float_as_uint(o.w) : 0u, __float_as_uint(iv.w));
-                steps = 0;
+                if (DIAG) steps = 0;
                 if (tr.mode == TM_DONE) finish(); else active = true;
             }
             chunk_next += min((uint32_t)__popcll(idle), avail);
@@ -1808,7 +1813,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 #endif
         if (active) {
             for (int k = 0; k < (OCC ? STEPS_PER_REFILL_SHADOW : STEPS_PER_REFILL); ++k) {
-                ++steps;
+                if (DIAG) ++steps;
                 if (!tr.step(sc, st)) { finish(); active = false; break; }
             }
         }
@@ -3567,8 +3572,11 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             }
         }
         b(RT_KERNEL_EXTEND);
-        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        if (diag) {
+            if (s->ds.listed_only) k_trace<false, true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+            else k_trace<false, false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        } else if (s->ds.listed_only) k_trace<false, true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        else k_trace<false, false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         if (env) {
             if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
@@ -3579,8 +3587,11 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-        else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        if (diag) {
+            if (s->ds.listed_only) k_trace<true, true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+            else k_trace<true, false, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        } else if (s->ds.listed_only) k_trace<true, true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        else k_trace<true, false, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
         e(RT_KERNEL_CONNECT);
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
@@ -4185,7 +4196,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("hipGetDeviceProperties"); return fail(RT_ERROR_DEVICE); }
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
         // Persistent trace blocks: 75 % of one full-occupancy wave of blocks (RT_TRACE_GRID_PCT).
         // Four partitions run their trace launches side by side; a full grid per launch left
