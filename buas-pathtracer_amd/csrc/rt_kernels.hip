@@ -1175,7 +1175,7 @@ struct Pool {
     float4* hit;         // t | code | tri | v
     float*  hit_w;       // a mesh hit's w (written by k_trace with the hit; read for mesh hits only)
     uint16_t* mstack;    // [64][n]
-    uint8_t*  state;     // S_FREE / S_TRACE / S_DONE per slot
+    uint8_t*  state;     // S_FREE / S_TRACE / S_DONE / S_NEW (a traced camera ray) per slot
     float4*   ext_rec[2];// extension queues (ping-pong), REC_Q float4 per ray: {o, slot}, {d, t after planes}, {1/d, -}
     // The shadow queue.  RT_SH_STAGE (default): k_shade writes a queued shadow ray's record and
     // contribution at its own slot as soon as the ray's prologue is done (so they are not held in
@@ -1211,7 +1211,13 @@ struct Pool {
 // Slot states.  Every per-iteration kernel except the tracers walks the pool in
 // slot order (thread i = slot i): the SoA loads coalesce, and the queues it
 // appends to come out as runs of consecutive slots (one run per wavefront).
-enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2 };
+enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2, S_NEW = 3 };
+// RT_GEN_LEAN (default): k_generate writes a new path as S_NEW without its throughput and
+// total_color records (1, 0 and the bounce-0 flags), and k_shade / k_drain make them from the
+// state, the vignette from the camera ray (new_path_records); 32 B per new path less to write.
+#ifndef RT_GEN_LEAN
+#define RT_GEN_LEAN 1
+#endif
 constexpr int REC_Q = 3;     // float4 per queued ray record
 #ifndef RT_SH_STAGE
 #define RT_SH_STAGE 1
@@ -1542,6 +1548,20 @@ __global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out
         out[base + local] = (min_x + local % tw) | ((min_y + local / tw) << 16);
 }
 
+// The vignette of a camera ray (RT/raytracer.cpp:451-453): k_generate stores it with the path, and
+// under RT_GEN_LEAN k_shade / k_drain recompute it from the stored direction (same operations, same bits).
+RT_D float camera_vignette(const FrameParams& fp, const rt_settings& st, V3 rd) {
+    float vig = dot(rd, fp.cz);
+    vig = vig*vig*vig*vig;
+    return lerpf_(1.0f, vig, st.vignette_strength);
+}
+// The throughput and total_color records of an S_NEW path (RT_GEN_LEAN), as k_generate would have
+// written them: throughput (1, 1, 1 | vignette), total_color (0, 0, 0 | bounce 0, specular)
+RT_D void new_path_records(const FrameParams& fp, const rt_settings& st, float4 d4, float4& t4, float4& L4) {
+    t4 = make_float4(1.0f, 1.0f, 1.0f, camera_vignette(fp, st, ld3(d4)));
+    L4 = make_float4(0.0f, 0.0f, 0.0f, __uint_as_float(pack_flags(0, 1, 0)));
+}
+
 // The AA jitter of sample s of pixel (x, y): render_tile's first sampler draw (RT/raytracer.cpp:
 // 431-435).  The sample's RandomSeries is seeded from its key and this draw comes first, so the
 // jitter is a function of the key: the splat recomputes it instead of carrying it with the path.
@@ -1643,19 +1663,19 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
         film_p = add(film_p, smul((v + pixel_h*jy)*hfh, fp.cy));
         V3 jcp = add(add(fp.cp, smul(djx, fp.cx)), smul(djy, fp.cy));
         V3 rd = normalize(sub(film_p, jcp));
-        float vig = dot(rd, fp.cz);
-        vig = vig*vig*vig*vig;
-        vig = lerpf_(1.0f, vig, st.vignette_strength);
+        const float vig = camera_vignette(fp, st, rd);
         nro = jcp; nrd = rd;
         pool.ray_o[slot] = make_float4(jcp.x, jcp.y, jcp.z, __uint_as_float(x | (y << 16)));
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
-        pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
         cast = st.max_bounce_count > 0;
-        pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, !cast ? vig : __uint_as_float(pack_flags(0, 1, 0)));
+        if (!RT_GEN_LEAN || !cast) {
+            pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
+            pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, !cast ? vig : __uint_as_float(pack_flags(0, 1, 0)));
+        }
         pool.prev_n[slot] = make_float2(0.0f, __uint_as_float(p));
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         // material_stack[0] = &air: level 0 is never stored; k_shade reads it as sc.air_id
-        pool.state[slot] = cast ? S_TRACE : S_DONE;      // max_bounce_count == 0: nothing to trace
+        pool.state[slot] = cast ? (RT_GEN_LEAN ? S_NEW : S_TRACE) : S_DONE;   // max_bounce_count == 0: nothing to trace
         if (cast) {
             pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false, 0u);
             pool.hit[slot] = make_float4(pro.t, __uint_as_float(pro.code), 0.0f, 0.0f);
@@ -2102,6 +2122,10 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         state0 = pool.state[slot];
         load_path();
     }
+    if (RT_GEN_LEAN && state0 == S_NEW) {                              // a camera ray (k_generate)
+        new_path_records(fp, st, d4, t4, L4);
+        state0 = S_TRACE;
+    }
     const DevScene sc = scene_in_lds<IN_LDS>(sc_g, lds_scene);
     const bool valid = slot < pool.n && state0 == S_TRACE;             // traced this iteration
     bool cont = false, done = false, shadow = false, cast_shadow = false, enq = false;
@@ -2343,7 +2367,8 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
 __global__ void __launch_bounds__(BLOCK) k_drain_list(Pool pool, Counters* cnt) {
     if (!cnt->fused || cnt->done) return;                              // uniform
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
-    const bool live = slot < pool.n && pool.state[slot] == S_TRACE;
+    const uint8_t stv = slot < pool.n ? pool.state[slot] : S_FREE;
+    const bool live = stv == S_TRACE || stv == S_NEW;
     if (slot < pool.n && (slot & 63u) == 0) pool.fin_w[slot >> 6] = 0;
     const uint32_t shard = blockIdx.x % NSHARD;
     __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
@@ -2421,9 +2446,10 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
             if (!active && rank < avail) {
                 slot = pool.sh_slot[chunk_next + rank];
                 const float4 o4 = ldnt(&pool.ray_o[slot]), d4 = ldnt(&pool.ray_d[slot]);
-                const float4 t4 = ldnt(&pool.thr[slot]), L4 = ldnt(&pool.L[slot]);
+                float4 t4 = ldnt(&pool.thr[slot]), L4 = ldnt(&pool.L[slot]);
                 const float2 pn2 = ldnt(&pool.prev_n[slot]);
                 const uint4 r4 = ldnt(&pool.rng[slot]);
+                if (RT_GEN_LEAN && pool.state[slot] == S_NEW) new_path_records(fp, st, d4, t4, L4);
                 ro = ld3(o4); rd = ld3(d4); thr = ld3(t4); total = ld3(L4); vig = t4.w;
                 prev_pdf = pn2.x; p = __float_as_uint(pn2.y);
                 const uint32_t flags = __float_as_uint(L4.w);
