@@ -1218,6 +1218,10 @@ enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2, S_NEW = 3 };
 #ifndef RT_GEN_LEAN
 #define RT_GEN_LEAN 1
 #endif
+// k_generate loads its claims and the claimed samples' pixels before it splats (see k_generate)
+#ifndef RT_GEN_HOIST
+#define RT_GEN_HOIST 1
+#endif
 constexpr int REC_Q = 3;     // float4 per queued ray record
 #ifndef RT_SH_STAGE
 #define RT_SH_STAGE 1
@@ -1591,40 +1595,25 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
-    if (lane < pool.fin_w[wbase]) {
-        const float4 fl = ldnt(&pool.fin_L[slot]);
-        const uint2 fk = ldnt(&pool.fin_k[slot]);
-        const uint32_t pixel = ldnt(&pool.fin_px[slot]);
-        const uint32_t s = fp.list_xy ? fp.list_s[fk.x] : fk.x;
-        const V2 j = sample_jitter(sc_g, st, fp, pixel & 0xFFFFu, pixel >> 16, s);
-        splat_sample(fp, pool, ld3(fl), fl.w, make_float2(j.x, j.y), fk.x, fk.y);
-    }
     // Each wave's survivors fill its first slots; the rest take new paths, claiming consecutive
     // sample numbers in slot order from the scan of the free counts k_bookkeep made (no atomics):
     // the block's first claim, the free slots of the block's earlier waves, the lane's rank.
+    // The claim and the claimed sample's pixel are loaded first (RT_GEN_HOIST), so their round trips
+    // overlap the splat's below instead of waiting behind its stores.
     const uint32_t first = 64u - pool.free_w[wbase];
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += pool.free_w[wbase - wave + w];
     const bool want = lane >= first;
-    const uint32_t claim = pool.claim_base[blockIdx.x] + before + (lane - first);
+    const uint32_t cbase = pool.claim_base[blockIdx.x];
+    const unsigned long long remaining = remaining_samples(cnt);
+    const uint32_t claim = cbase + before + (lane - first);
     // No sample left for this block to claim (the frame's drain): its free slots go idle
-    if ((unsigned long long)pool.claim_base[blockIdx.x] >= remaining_samples(cnt)) {
-        if (want) pool.state[slot] = S_FREE;
-        return;
-    }
-#if RT_GEN_LDS_SCENE
-    const DevScene sc = scene_in_lds(sc_g, lds_scene);
-#else
-    const DevScene& sc = sc_g;       // nothing generate reads lives in the LDS copy (see RT_GEN_LDS_SCENE)
-#endif
-    const bool active = want && (unsigned long long)claim < remaining_samples(cnt);
-    if (want && !active) pool.state[slot] = S_FREE;
-    bool enqueue = false, cast = false;
-    V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
-    Prologue pro = {};
+    const bool none_left = (unsigned long long)cbase >= remaining;
+    const bool active = !none_left && want && (unsigned long long)claim < remaining;
+    const unsigned long long k = cnt->next_sample + claim;
+    uint32_t x = 0, y = 0, s = 0, p = 0;
+#if RT_GEN_HOIST
     if (active) {
-        unsigned long long k = cnt->next_sample + claim;
-        uint32_t x, y, s, p = 0;
         if (fp.list_xy) {
             x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
         } else {
@@ -1639,6 +1628,48 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
             const uint32_t xy = fp.pix_xy[p];                // the tile list's pixel p (k_pixel_map)
             x = xy & 0xFFFFu; y = xy >> 16; s = pass;
         }
+    }
+#endif
+    // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
+    // splat them.  Their NEE contributions from k_connect are in by now.
+    if (lane < pool.fin_w[wbase]) {
+        const float4 fl = ldnt(&pool.fin_L[slot]);
+        const uint2 fk = ldnt(&pool.fin_k[slot]);
+        const uint32_t pixel = ldnt(&pool.fin_px[slot]);
+        const uint32_t fs = fp.list_xy ? fp.list_s[fk.x] : fk.x;
+        const V2 j = sample_jitter(sc_g, st, fp, pixel & 0xFFFFu, pixel >> 16, fs);
+        splat_sample(fp, pool, ld3(fl), fl.w, make_float2(j.x, j.y), fk.x, fk.y);
+    }
+    if (none_left) {
+        if (want) pool.state[slot] = S_FREE;
+        return;
+    }
+#if RT_GEN_LDS_SCENE
+    const DevScene sc = scene_in_lds(sc_g, lds_scene);
+#else
+    const DevScene& sc = sc_g;       // nothing generate reads lives in the LDS copy (see RT_GEN_LDS_SCENE)
+#endif
+    if (want && !active) pool.state[slot] = S_FREE;
+    bool enqueue = false, cast = false;
+    V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
+    Prologue pro = {};
+    if (active) {
+#if !RT_GEN_HOIST
+        if (fp.list_xy) {
+            x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
+        } else {
+            uint32_t pass;
+            if (k < 0x100000000ull && fp.px_m) {             // a multiply-high when k fits 32 bits
+                pass = div_pixels((uint32_t)k, fp.px_m);
+                p = (uint32_t)k - pass*fp.pixels;
+            } else {
+                pass = (uint32_t)(k / fp.pixels);
+                p = (uint32_t)(k % fp.pixels);
+            }
+            const uint32_t xy = fp.pix_xy[p];                // the tile list's pixel p (k_pixel_map)
+            x = xy & 0xFFFFu; y = xy >> 16; s = pass;
+        }
+#endif
         uint32_t canonical = fp.frame_count + s;
         uint32_t tile = tile_of(fp, x, y);
         Rng rng = random_seed(sample_seed(fp.total_frame_index, fp.frame_count, tile, y*fp.w + x, canonical));
