@@ -3151,6 +3151,7 @@ struct rt_scene {
     uint32_t trace_grid = 0;        // persistent k_trace blocks (extend)
     uint32_t connect_grid = 0;      // persistent k_trace<true> blocks (<= trace_grid: the spill area)
     uint32_t drain_grid = 0;        // persistent k_drain blocks (<= trace_grid: the spill area)
+    uint32_t drain_lanes_full = 0;  // k_drain lanes of a grid that fills the GPU (the fused-drain threshold's unit)
     float4* d_samp = nullptr;       // per-sample records for the deterministic splat
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
@@ -3520,7 +3521,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     // rt_scene_config::fuse_paths another count (0 = never)
     const uint32_t fuse_paths = s->cfg.fuse_paths >= 0
         ? (uint32_t)std::min<int64_t>(s->cfg.fuse_paths, 0xFFFFFFFFll)
-        : std::max(s->drain_grid*DTB*5u/2u, pool_n / 10u);
+        : std::max(s->drain_lanes_full*5u/2u, pool_n / 10u);
     for (int k = 0; k < nparts; ++k) {
         int err = ensure_partition(s, k);
         if (!err) err = ensure_pool(s->part[k], pool_n);
@@ -4276,6 +4277,9 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             drain_cu = 1;
         // (lanes <= the trace grid's: the spill area is sized for those)
         s->drain_grid = std::min(s->trace_grid*(uint32_t)(TB / DTB), (uint32_t)(prop.multiProcessorCount*drain_cu));
+        s->drain_lanes_full = s->drain_grid*DTB;
+        if (const char* e = getenv("RT_DRAIN_GRID_PCT"))
+            s->drain_grid = std::max(1u, (uint32_t)((unsigned long long)s->drain_grid*(unsigned)std::max(1, atoi(e)) / 100ull));
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }

@@ -6,7 +6,7 @@
 # after the summary and the traces gzipped, so gpurun_out stays under the 64 MiB copy-back limit.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_r03
+OUT=gpurun_out/${PROF_TAG:-prof_r03}
 mkdir -p $OUT
 cp profiles/traffic.json $OUT/traffic.json
 for c in ${CONFIGS:-c3 c4 c5}; do
@@ -22,11 +22,11 @@ for c in ${CONFIGS:-c3 c4 c5}; do
   python3 tools/timeline.py "$tr" > $OUT/${c}_timeline.txt 2>&1
   gzip -c "$tr" > $OUT/${c}_kernel_trace.csv.gz; rm -rf $OUT/kt_$c
   echo "trace $c: $(grep -E '^frame' $OUT/${c}_timeline.txt)"
-  TAG=prof_r03/pmc_$c PMC_BENCH="$pm --no-cpu-baseline --c4-steps 0" tools/gpu_pmc_full.sh || { echo "pmc $c failed"; exit 1; }
-  python3 tools/pmc_summary.py gpurun_out/prof_r03/pmc_$c --out $OUT/${c}_pmc.md --traffic $OUT/traffic.json --config $c \
-      --bench-log gpurun_out/prof_r03/pmc_$c/pass1.log > /dev/null
-  cp gpurun_out/prof_r03/pmc_$c/pass1.log $OUT/${c}_pmc_bench.log
-  rm -rf gpurun_out/prof_r03/pmc_$c/pass*/
+  TAG=${PROF_TAG:-prof_r03}/pmc_$c PMC_BENCH="$pm --no-cpu-baseline --c4-steps 0" tools/gpu_pmc_full.sh || { echo "pmc $c failed"; exit 1; }
+  python3 tools/pmc_summary.py $OUT/pmc_$c --out $OUT/${c}_pmc.md --traffic $OUT/traffic.json --config $c \
+      --bench-log $OUT/pmc_$c/pass1.log > /dev/null
+  cp $OUT/pmc_$c/pass1.log $OUT/${c}_pmc_bench.log
+  rm -rf $OUT/pmc_$c/pass*/
   echo "pmc $c: summarised"
 done
 rm -rf gpurun_out/assets
