@@ -12,7 +12,11 @@
 #include <stdint.h>
 #include "../../include/rt_abi.h"
 
+#ifdef RT_DMATH_HOST_TEST        // tools/check_sincos.cpp: the device math compiled for the host
+#define RT_D inline
+#else
 #define RT_D __device__ __forceinline__
+#endif
 
 namespace rtd {
 
@@ -136,6 +140,31 @@ RT_D float d_cosf(float xx) {
     float z = x * x;
     float r = (j == 1u || j == 2u) ? sin_poly(x, z) : cos_poly(z);
     return sgn ? -r : r;
+}
+// sin and cos of one argument (map_to_hemisphere, the bokeh sample): one range reduction and one
+// evaluation of each polynomial for both, the same operations as d_sinf / d_cosf, so the same bits
+// (a -0 argument reduces to +0 here, where d_sinf keeps -0; both give sin(-0) = +0 through sin_poly)
+RT_D void d_sincosf(float xx, float& s_out, float& c_out) {
+    const float x0 = fabsf(xx);
+    if (!(x0 < 8192.0f)) {
+        s_out = (xx == xx) ? 0.0f : xx;
+        c_out = (x0 == x0) ? 1.0f : x0;
+        return;
+    }
+    uint32_t j = (uint32_t)(FOPI * x0);
+    float y = (float)j;
+    if (j & 1u) { j += 1u; y += 1.0f; }
+    j &= 7u;
+    int ss = xx < 0.0f ? 1 : 0, cs = 0;
+    if (j > 3u) { j -= 4u; ss ^= 1; cs ^= 1; }
+    if (j > 1u) cs ^= 1;
+    const float x = ((x0 - y * DP1) - y * DP2) - y * DP3;
+    const float z = x * x;
+    const float sp = sin_poly(x, z), cp = cos_poly(z);
+    const bool swap = j == 1u || j == 2u;
+    const float rs = swap ? cp : sp, rc = swap ? sp : cp;
+    s_out = ss ? -rs : rs;
+    c_out = cs ? -rc : rc;
 }
 RT_D float d_ldexp(float y, int n) {
     if (n > 127) { y = y * __uint_as_float(0x7F000000u); n -= 127; if (n > 127) n = 127; }

@@ -971,6 +971,14 @@ RT_D float sample_1d(const DevScene& sc, const SamplerState& s, Rng& rng, int di
 // ======================================================================
 // Integrator helpers (RT/integrators.cpp)
 // ======================================================================
+// d_sincosf in the indirect bounce's hemisphere sample; the NEE light sample keeps the two calls
+// (there the fused form's two live results cost k_shade 8 B of scratch at 64 VGPRs)
+#ifndef RT_SINCOS_NEE
+#define RT_SINCOS_NEE 0
+#endif
+#ifndef RT_SINCOS_IND
+#define RT_SINCOS_IND 1
+#endif
 RT_D V3 random_in_unit_sphere(Rng& e) {                                   // :11-19
     V3 r;
     int guard = 0;   // bounded (a degenerate all-zero RandomSeries would spin forever)
@@ -992,13 +1000,25 @@ RT_D V3 oriented_around_normal(V3 v, V3 n) {                             // :58-
 RT_D V3 map_to_hemisphere(V3 N, V2 rs) {                                 // :93-105
     float az = TAU_32*rs.x, y = rs.y;
     float s = __builtin_sqrtf(1.0f - y*y);
+#if RT_SINCOS_NEE
+    float sa, ca;
+    d_sincosf(az, sa, ca);                          // = d_sinf(az), d_cosf(az), bit for bit
+    V3 h = {ca*s, y, sa*s};
+#else
     V3 h = {d_cosf(az)*s, y, d_sinf(az)*s};
+#endif
     return oriented_around_normal(h, N);
 }
 RT_D V3 map_to_cosine_weighted_hemisphere(V3 N, V2 rs) {                 // :107-119
     float az = TAU_32*rs.x, y = rs.y;
     float s = __builtin_sqrtf(1.0f - y);
+#if RT_SINCOS_IND
+    float sa, ca;
+    d_sincosf(az, sa, ca);
+    V3 h = {ca*s, __builtin_sqrtf(y), sa*s};
+#else
     V3 h = {d_cosf(az)*s, __builtin_sqrtf(y), d_sinf(az)*s};
+#endif
     return oriented_around_normal(h, N);
 }
 RT_D float fresnel_dielectric(float ci, float ei, float et, float eta, float& co) {   // :235-258
@@ -1043,8 +1063,10 @@ RT_D V3 env_direction(const DevScene& sc, float e, V2 s2) {
     const float u = ((float)x0 + s2.x*(float)cw) / (float)sc.sky_w;
     const float v = ((float)y0 + s2.y*(float)ch) / (float)sc.sky_h;
     const float phi = (u - 0.5f)*(2.0f*PI_32), theta = (v - 0.5f)*PI_32;   // sample_sky's mapping inverted
-    const float ct = d_cosf(theta);
-    return {ct*d_cosf(phi), d_sinf(theta), ct*d_sinf(phi)};
+    float st, ct, sp, cp;
+    d_sincosf(theta, st, ct);
+    d_sincosf(phi, sp, cp);
+    return {ct*cp, st, ct*sp};
 }
 // sample_sky's texel for d, and the table tile it lies in
 RT_D V3 sky_env(const DevScene& sc, V3 d, uint32_t& tile) {
@@ -1441,7 +1463,9 @@ RT_D V2 transform_bokeh_sample(V2 o, float f, float n, float phi_shutter_max) {
     } else {
         phir.y *= 1.0f;
     }
-    return {d_cosf(phir.x)*phir.y, d_sinf(phir.x)*phir.y};
+    float sp, cp;
+    d_sincosf(phir.x, sp, cp);
+    return {cp*phir.y, sp*phir.y};
 }
 RT_D V2 brown_conrady(V2 uv, float amount, float woh) {
     uv.y /= woh;

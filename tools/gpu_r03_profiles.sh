@@ -8,7 +8,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${PROF_TAG:-prof_r03}
 mkdir -p $OUT
-cp profiles/traffic.json $OUT/traffic.json
+[ -f $OUT/traffic.json ] || cp profiles/traffic.json $OUT/traffic.json   # a later call adds its configs
 for c in ${CONFIGS:-c3 c4 c5}; do
   case $c in
     c3) kt="--steps 3 --warmup 1"; pm="--steps 1 --warmup 0" ;;
