@@ -2738,13 +2738,24 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
 //
 // Partition k resolves its own pass range into its own buffer (the caller's for k = 0),
 // so partitions never write the same buffer; k_combine_partials adds them up at the end.
+// RT_RES_PREFETCH 1: the next pass's records load into registers while this pass is summed (r02-r03;
+// 120 VGPRs); 0 (default, r03b) loads each pass at its start: 90 VGPRs, and the blocks find room
+// beside the other partitions' kernels sooner (C3 +0.2 %, C4 +0.6 %), the load latency exposed per pass
+#ifndef RT_RES_PREFETCH
+#define RT_RES_PREFETCH 0
+#endif
 constexpr int TR_W = 64, TR_H = 16, TR_THREADS = 256, TR_ROWS = TR_H / (TR_THREADS / TR_W);
 __host__ __device__ constexpr int tr_stage_slots(int ks) { return ((TR_W + 2*ks)*(TR_H + 2*ks) + TR_THREADS - 1) / TR_THREADS; }
 __host__ __device__ constexpr size_t tr_lds_bytes(int ks) {
     return (size_t)(TR_W + 2*ks)*(TR_H + 2*ks)*(16 + 4) + 512*4;
 }
+#ifdef RT_RES_WAVES
+#define RT_RES_ATTR __attribute__((amdgpu_waves_per_eu(RT_RES_WAVES)))
+#else
+#define RT_RES_ATTR
+#endif
 template <int KSMAX>
-__global__ void __launch_bounds__(TR_THREADS) k_resolve_tiles(FrameParams fp, Pool pool, const Counters* cnt,
+__global__ void __launch_bounds__(TR_THREADS) RT_RES_ATTR k_resolve_tiles(FrameParams fp, Pool pool, const Counters* cnt,
                                                                const uint32_t* blocks, float4* dst) {
     const uint32_t s0 = cnt->res_from, s1 = cnt->res_to;
     if (s0 >= s1) return;
@@ -2807,8 +2818,13 @@ __global__ void __launch_bounds__(TR_THREADS) k_resolve_tiles(FrameParams fp, Po
     const float kscale = ks ? (float)(fp.cache_size - 1) / (float)ks : 0.0f;
     const int xa = max(X - ks, 0), xb = min(X + ks, W - 1);
     const int ya = max(Y0 - ks, 0), yb = min(Y0 + TR_ROWS - 1 + ks, H - 1);
+#if RT_RES_PREFETCH
     load_pass(s0);
+#endif
     for (uint32_t s = s0; s < s1; ++s) {
+#if !RT_RES_PREFETCH
+        load_pass(s);
+#endif
         __syncthreads();                                    // the previous pass's sums are done with LDS
 #pragma unroll
         for (int k = 0; k < NST; ++k) {
@@ -2816,7 +2832,9 @@ __global__ void __launch_bounds__(TR_THREADS) k_resolve_tiles(FrameParams fp, Po
             if (i < N) { srgb[i] = pc[k]; sjy[i] = pj[k]; }
         }
         __syncthreads();
+#if RT_RES_PREFETCH
         if (s + 1 < s1) load_pass(s + 1);                   // in flight while this pass is summed
+#endif
         if (!col_in) continue;
         for (int sy = ya; sy <= yb; ++sy) {
             const int rlo = max(sy - ks - Y0, 0), rhi = min(sy + ks - Y0, TR_ROWS - 1);
