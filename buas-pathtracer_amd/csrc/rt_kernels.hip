@@ -1267,7 +1267,7 @@ struct Counters {
     uint32_t ext_count[2][NSHARD][LINE_WORDS];   // extension queue length per shard (ping-pong)
     uint32_t shadow_count[NSHARD][LINE_WORDS];   // shadow queue length per shard
     uint32_t fetch[2][NSHARD][LINE_WORDS];       // persistent trace kernels: items handed out (extend, connect)
-    uint32_t cast[2][NSHARD][LINE_WORDS];        // rays cast this iteration: [0] new paths (k_generate), [1] shadow
+    uint32_t cast[2][NSHARD][LINE_WORDS];        // rays cast this iteration: [1] shadow (k_shade); [0] unused since r03 (k_bookkeep counts the camera rays from the claims)
     uint32_t alive[NSHARD][LINE_WORDS];          // paths k_shade continued (each casts a closest ray next iteration)
     uint32_t unsplat[NSHARD][LINE_WORDS];        // paths finished this iteration, splatted by the next k_generate
     uint32_t gen_free;              // free slots counted by the last k_bookkeep = claims of the next k_generate
@@ -1739,11 +1739,11 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     }
     // new paths that enter the BVH go to the current extension queue behind the survivors
     const uint32_t shard = blockIdx.x % NSHARD;
-    __shared__ uint32_t tally[(BLOCK / 64 + 2)*2];
-    const bool tp[2] = {enqueue, cast};
-    uint32_t* const tc[2] = {&cnt->ext_count[cur][shard][0], &cnt->cast[0][shard][0]};
-    uint32_t tpos[2], ttot[2];
-    block_tally<BLOCK, 2>(tp, tc, tpos, ttot, tally);
+    __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
+    const bool tp[1] = {enqueue};
+    uint32_t* const tc[1] = {&cnt->ext_count[cur][shard][0]};
+    uint32_t tpos[1], ttot[1];
+    block_tally<BLOCK, 1>(tp, tc, tpos, ttot, tally);
     const uint32_t pos = tpos[0];
     if (enqueue) {
         float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + pos);
@@ -2903,11 +2903,25 @@ __global__ void __launch_bounds__(256) k_combine_partials(float4* accum, const f
 enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
 // fuse: set Counters::fused once nothing is left to claim and at most this many paths are alive
 // (0: never; see k_drain)
-struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse; };
+// cast0: max_bounce_count > 0, so every sample claimed this iteration casts a camera ray (k_bookkeep counts
+// them from the claims; k_generate keeps no counter for them)
+struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0; };
+// Two workgroup sizes, picked per frame by the partition's pool (RT_BK_LARGE_POOL): a pool of 4M paths or
+// more (a whole 1080p frame: 8.4M) takes the 256-thread build (156 VGPRs: 4 waves that find room beside
+// the other partitions' kernels sooner), a smaller one (a rank's share of a multi-GPU frame: 3.3M) the
+// 1024-thread build (62 VGPRs, 16 waves on one CU).  A/B (profiles/r03b_ab.txt section 14): 256 threads
+// give the full C3 frame +0.5 to +0.9 % and C4 +1.2 to +1.5 %, but rank 0 of 8 -1.9 to -2.8 %.
 #ifndef RT_BK_THREADS
 #define RT_BK_THREADS 1024
 #endif
-constexpr int BK_THREADS = RT_BK_THREADS;
+#ifndef RT_BK_THREADS_LARGE
+#define RT_BK_THREADS_LARGE 256
+#endif
+#ifndef RT_BK_LARGE_POOL
+#define RT_BK_LARGE_POOL (4u << 20)
+#endif
+constexpr int BK_THREADS_SMALL = RT_BK_THREADS, BK_THREADS_LARGE = RT_BK_THREADS_LARGE;
+template <int BK_THREADS>
 __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
                                                          ResPlan plan) {
     __shared__ uint32_t sc[BK_THREADS];
@@ -2940,9 +2954,8 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         // partitions' kernels, 10 % of a partition's iteration.)
         const bool it_phase = phase == BK_ITER;
         const uint32_t done_flag = it_phase ? cnt->done : 0u;
-        uint32_t c0 = 0, al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
+        uint32_t al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
         if (it_phase && t < NSHARD) {
-            c0 = cnt->cast[0][t][0];
             al = cnt->alive[t][0];
             c1 = cnt->cast[1][t][0];
             us = cnt->unsplat[t][0];
@@ -2961,7 +2974,6 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         const bool sk = it_phase && done_flag;
         if (it_phase && !sk && t < NSHARD) {
             cnt->unsplat[t][0] = 0;
-            cnt->cast[0][t][0] = 0;
             cnt->cast[1][t][0] = 0;
             cnt->alive[t][0] = 0;
             cnt->ext_count[cur][t][0] = 0;
@@ -2969,7 +2981,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             cnt->fetch[0][t][0] = 0;
             cnt->fetch[1][t][0] = 0;
         }
-        uint32_t ext = c0 + al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
+        uint32_t ext = al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
 #pragma unroll
         for (int off = 1; off < NSHARD; off <<= 1) {
             ext += __shfl_xor(ext, off); sh += __shfl_xor(sh, off); pend += __shfl_xor(pend, off);
@@ -2981,9 +2993,12 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             if (it_phase && !sk) {
                 const unsigned long long lm = lim < total ? lim : total;
                 const unsigned long long rem = lm > next ? lm - next : 0ull;      // remaining_samples()
-                next += ((unsigned long long)gfree < rem ? (unsigned long long)gfree : rem);
+                const unsigned long long claimed = (unsigned long long)gfree < rem ? (unsigned long long)gfree : rem;
+                next += claimed;
                 cnt->next_sample = next;
-                cnt->closest_rays += ext;
+                // the camera rays of this iteration's k_generate: one per claimed sample (every claim below
+                // the remaining count becomes a path, k_generate) when max_bounce_count > 0
+                cnt->closest_rays += ext + (plan.cast0 ? claimed : 0ull);
                 cnt->shadow_rays += sh;
                 cnt->traced_rays[0] += tq;
                 cnt->traced_rays[1] += ts;
@@ -3543,6 +3558,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     const FrameShape shape = frame_shape(s, total, listed ? 0u : sp.passes);
     const int nparts = shape.nparts;
     const uint32_t pool_n = shape.pool_n;
+    // k_bookkeep's workgroup size by the pool (RT_BK_LARGE_POOL, see k_bookkeep)
+    const bool bk_large = pool_n >= RT_BK_LARGE_POOL;
+    auto launch_bookkeep = [bk_large](Counters* c, const Pool& pl, uint32_t nblocks, int cur, int phase, ResPlan plan,
+                                      hipStream_t q) {
+        if (bk_large) k_bookkeep<BK_THREADS_LARGE><<<1, BK_THREADS_LARGE, 0, q>>>(c, pl, nblocks, cur, phase, plan);
+        else k_bookkeep<BK_THREADS_SMALL><<<1, BK_THREADS_SMALL, 0, q>>>(c, pl, nblocks, cur, phase, plan);
+    };
     const bool stream_splat = !listed && sp.mode == RT_SPLAT_STREAM;
     const size_t npx = (size_t)fp.w*fp.h;
     const uint32_t prof = g_profiling & ~(1u << RT_KERNEL_SPLAT);   // the splat runs inside k_generate
@@ -3611,7 +3633,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
         HIP_OK(hipMemsetAsync(pt.pool.fin_w, 0, 4ull*N / 64, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_w, 64, N / 64, r.stream));
-        k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{});
+        launch_bookkeep(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{}, r.stream);
         if (prof && !pt.events) {
             for (auto& e : pt.ev) HIP_OK(hipEventCreate(&e));
             for (auto& e : pt.ev_final) HIP_OK(hipEventCreate(&e));
@@ -3620,7 +3642,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     }
     auto plan_of = [&](int k, uint32_t mode) {
         const Run& r = run[k];
-        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, life, fuse_paths};
+        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, life, fuse_paths, st->max_bounce_count > 0 ? 1u : 0u};
     };
     // Stage timing without extra host syncs: each iteration records begin/end
     // events into one of EV_SLOTS ring slots; a chunk's slots are read back when
@@ -3696,7 +3718,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
         const bool res = stream_splat && (plan || r.drain);
-        k_bookkeep<<<1, BK_THREADS, 0, q>>>(pt.cnt, pv, r.grid, r.cur, BK_ITER, plan_of(k, res ? 1u : 0u));
+        launch_bookkeep(pt.cnt, pv, r.grid, r.cur, BK_ITER, plan_of(k, res ? 1u : 0u), q);
         r.res_ev[slot] = res && ((prof >> RT_KERNEL_RESOLVE) & 1u);
         if (res) {                       // the passes the bookkeep found complete, if enough of them
             b(RT_KERNEL_RESOLVE);
@@ -3728,7 +3750,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if (!stream_splat) return RT_OK;
         Partition& pt = s->part[k];
         Run& r = run[k];
-        k_bookkeep<<<1, BK_THREADS, 0, r.stream>>>(pt.cnt, pt.pool, r.grid, r.cur, BK_FINAL, plan_of(k, 2u));
+        launch_bookkeep(pt.cnt, pt.pool, r.grid, r.cur, BK_FINAL, plan_of(k, 2u), r.stream);
         const bool t = (prof >> RT_KERNEL_RESOLVE) & 1u;
         if (t) HIP_OK(hipEventRecord(pt.ev_final[0], r.stream));
         launch_resolve_tiles(sp, fp, pt.pool, pt.cnt, r.dst, r.stream);
