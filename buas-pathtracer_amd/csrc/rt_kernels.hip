@@ -2938,7 +2938,11 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
     // The free counts' loads go out first, so they overlap the counter work below.
     // Up to BK_EMAX entries per thread (pools up to 32k blocks, 8.4M paths) are loaded at once into
     // registers, all in flight, and the claims are written from them; a loop covers larger pools.
-    constexpr uint32_t BK_EMAX = 32*(1024 / BK_THREADS);
+#ifndef RT_BK_REG
+#define RT_BK_REG 1
+#endif
+    // RT_BK_REG 0: no register copy (two passes over the counts, the second from L2)
+    constexpr uint32_t BK_EMAX = RT_BK_REG ? 32*(1024 / BK_THREADS) : 1;
     const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
     const uint32_t lo = t*E, hi = min(lo + E, nblocks);
     uint32_t v[BK_EMAX];
