@@ -1612,12 +1612,20 @@ RT_D V2 sample_jitter(const DevScene& sc, const rt_settings& st, const FramePara
 constexpr uint32_t GEN_LDS_Q_SCALE = RT_GEN_LDS_SCENE ? 16u : 0u;   // dynamic LDS bytes per blob float4
 
 // k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
-__global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
-                                                    Counters* cnt, int cur) {
+// RT_GEN_BLOCK: k_generate's workgroup (a divisor of BLOCK).  Claims stay per BLOCK-slot group (the
+// scan k_bookkeep makes over k_shade's blocks): a wave's claims start at its group's claim_base plus the
+// free slots of the group's earlier waves, whichever workgroup they are in.
+#ifndef RT_GEN_BLOCK
+#define RT_GEN_BLOCK BLOCK
+#endif
+constexpr int GEN_BLOCK = RT_GEN_BLOCK;
+static_assert(BLOCK % GEN_BLOCK == 0 && GEN_BLOCK % 64 == 0, "k_generate's workgroup divides BLOCK");
+__global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
+                                                        Counters* cnt, int cur) {
     // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
     // splat them.  Their NEE contributions from k_connect are in by now.
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
-    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    const uint32_t lane = __lane_id(), wave = (slot >> 6) & (uint32_t)(BLOCK / 64 - 1);   // wave in the group
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
     // Each wave's survivors fill its first slots; the rest take new paths, claiming consecutive
     // sample numbers in slot order from the scan of the free counts k_bookkeep made (no atomics):
@@ -1628,7 +1636,7 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += pool.free_w[wbase - wave + w];
     const bool want = lane >= first;
-    const uint32_t cbase = pool.claim_base[blockIdx.x];
+    const uint32_t cbase = pool.claim_base[slot / BLOCK];
     const unsigned long long remaining = remaining_samples(cnt);
     const uint32_t claim = cbase + before + (lane - first);
     // No sample left for this block to claim (the frame's drain): its free slots go idle
@@ -1739,11 +1747,11 @@ __global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings s
     }
     // new paths that enter the BVH go to the current extension queue behind the survivors
     const uint32_t shard = blockIdx.x % NSHARD;
-    __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
+    __shared__ uint32_t tally[(GEN_BLOCK / 64 + 2)*1];
     const bool tp[1] = {enqueue};
     uint32_t* const tc[1] = {&cnt->ext_count[cur][shard][0]};
     uint32_t tpos[1], ttot[1];
-    block_tally<BLOCK, 1>(tp, tc, tpos, ttot, tally);
+    block_tally<GEN_BLOCK, 1>(tp, tc, tpos, ttot, tally);
     const uint32_t pos = tpos[0];
     if (enqueue) {
         float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + pos);
@@ -3685,7 +3693,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         // iteration after k_bookkeep set Counters::fused, whose extend / shade / connect then exit
         const int fuse = (r.near && fuse_paths) ? 1 : 0;
         b(RT_KERNEL_GENERATE);
-        k_generate<<<r.grid, BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
+        k_generate<<<r.grid*(BLOCK / GEN_BLOCK), GEN_BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE);
         if (fuse) {
             k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
