@@ -1261,7 +1261,12 @@ constexpr uint32_t SH_FIN = 0x80000000u;   // Pool::sh_slot: the shadow ray's pa
 // Queues and fetch heads are sharded NSHARD ways (shard = blockIdx % NSHARD, the
 // blocks that share an XCD), each counter on a 128-B line of its own: one word
 // saturates at ~88 returning atomics/us, and a 2M-slot pool has 4096 blocks.
-constexpr int NSHARD = 8;
+#ifndef RT_NSHARD
+#define RT_NSHARD 8
+#endif
+constexpr int NSHARD = RT_NSHARD;
+static_assert(NSHARD <= 64 && (NSHARD & (NSHARD - 1)) == 0, "k_bookkeep sums the shards in one wave");
+constexpr int NXCD = 8;                        // MI355X: workgroups are dealt round robin over 8 XCDs
 constexpr int LINE_WORDS = 32;
 struct Counters {
     uint32_t ext_count[2][NSHARD][LINE_WORDS];   // extension queue length per shard (ping-pong)
@@ -4643,11 +4648,11 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
                     // run x holds column-major positions [n*x/8, n*(x+1)/8); its k-th block goes to list
                     // position 8k + x (in the last round, when the runs differ by one, in order)
                     const size_t n = colmajor.size();
-                    std::vector<size_t> start(NSHARD + 1);
-                    for (int x = 0; x <= NSHARD; ++x) start[x] = n*(size_t)x / NSHARD;
+                    std::vector<size_t> start(NXCD + 1);
+                    for (int x = 0; x <= NXCD; ++x) start[x] = n*(size_t)x / NXCD;
                     blocks.clear();
                     for (size_t k = 0; blocks.size() < n; ++k)
-                        for (int x = 0; x < NSHARD; ++x)
+                        for (int x = 0; x < NXCD; ++x)
                             if (start[x] + k < start[x + 1]) blocks.push_back(colmajor[start[x] + k]);
                 }
                 const size_t aux = blocks.size() + 2*MAX_PARTITIONS;       // the pointer table, then the blocks
