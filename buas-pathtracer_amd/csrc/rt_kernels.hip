@@ -1796,6 +1796,9 @@ constexpr int STEPS_PER_REFILL_SHADOW = RT_STEPS_PER_REFILL_SHADOW;
 #define RT_TRACE_WAVES 4
 #endif
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
+#ifndef RT_TRACE_PRIO
+#define RT_TRACE_PRIO 1
+#endif
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
@@ -1805,9 +1808,10 @@ template <bool OCC, bool LST, bool DIAG>
 __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag,
                                                               int fuse) {
     if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
-#ifdef RT_TRACE_PRIO
+#if RT_TRACE_PRIO
     // trace waves are latency bound and issue little; shade waves sharing the SIMD are
-    // issue bound: let a trace wave's next load go out first
+    // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
+    // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
     __builtin_amdgcn_s_setprio(RT_TRACE_PRIO);
 #endif
     __shared__ uint2 lds_stack[STACK_LDS*TB];
