@@ -1244,6 +1244,12 @@ enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2, S_NEW = 3 };
 #ifndef RT_GEN_HOIST
 #define RT_GEN_HOIST 1
 #endif
+#ifndef RT_GEN_PRIO
+#define RT_GEN_PRIO 0
+#endif
+#ifndef RT_DRAIN_PRIO
+#define RT_DRAIN_PRIO 0
+#endif
 constexpr int REC_Q = 3;     // float4 per queued ray record
 #ifndef RT_SH_STAGE
 #define RT_SH_STAGE 1
@@ -1629,6 +1635,9 @@ __global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settin
                                                         Counters* cnt, int cur) {
     // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
     // splat them.  Their NEE contributions from k_connect are in by now.
+#if RT_GEN_PRIO
+    __builtin_amdgcn_s_setprio(RT_GEN_PRIO);        // measurement switch: generate waves' issue priority
+#endif
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const uint32_t lane = __lane_id(), wave = (slot >> 6) & (uint32_t)(BLOCK / 64 - 1);   // wave in the group
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
@@ -2466,6 +2475,9 @@ template <bool LST, bool ENV>
 __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
                                                uint2* spill) {
     if (!cnt->fused || cnt->done) return;                              // uniform
+#if RT_DRAIN_PRIO
+    __builtin_amdgcn_s_setprio(RT_DRAIN_PRIO);      // measurement switch: drain waves' issue priority
+#endif
     __shared__ uint2 lds_stack[STACK_LDS*DTB];
     Stack stk;
     stk.lds = lds_stack; stk.spill = spill; stk.lane = threadIdx.x; stk.block = DTB;
