@@ -5,14 +5,19 @@ BASELINE.json metric: "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU
 scaling".  The default workload is configs[2] (C3: Cornell box + ~70k-tri
 synthetic mesh with SAH BVH + synthetic 2048x1024 HDR environment + NEE + RR,
 1920x1080, 256 spp, max depth 12) — the 1-GPU configuration the metric is
-quoted on.  One step = one full frame of that workload: every tile of this
-rank's shard (tile t on rank t % N) integrated at 256 spp into an fp32 float4
-accumulation buffer already resident in HBM, plus (N > 1) the RCCL sum-reduce
-of the framebuffer over xGMI.  Strong scaling: the frame is fixed, the tiles
-are split over the ranks.
+quoted on.  One step = one full frame of that workload: this rank's share of
+the frame integrated into an fp32 float4 accumulation buffer already resident
+in HBM, plus (N > 1) the RCCL sum-reduce of the framebuffer over xGMI.  A
+rank's share is, by default, sample passes [spp*r/N, spp*(r+1)/N) of every
+tile (--shard-mode passes: equal cost per rank whatever the content); with
+--shard-mode tiles it is the tiles t % N (the reference's 64x64 tile queue
+dealt round robin).  Strong scaling: the frame is fixed, the work is split
+over the ranks.  The JSON's `c4` object times the north star's own scene
+(C4) on the same ranks.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+    python -m torch.distributed.run --nproc-per-node 1 ... bench.py --force-dist   (the RCCL path at one rank)
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel: the stage
 with the most GPU time in the timed region (k_shade on C3), algorithmic bytes =
@@ -22,7 +27,10 @@ launched it.  Four partitions run concurrently, so the launch
 time includes shared GPU time: `concurrency` gives the mean number of kernels in
 flight, `isolated` the serialized figures from the rocprofv3 --pmc runs, and
 `pipeline` the whole-frame figure of SURVEY.md §8(d) (152 B per ray + 144 B per
-sample over wall time).  `cpu_baseline` is the CPU restatement (oracle/,
+sample over wall time), and `traversal` the trace kernels' step fetches (128 B per
+step, the timed frames' own rt_stats::trace_steps) over their launch time.  The
+frame's TraversalStats (rt_stats::traversal, the reference's per-frame counters)
+are in `traversal_stats`.  `cpu_baseline` is the CPU restatement (oracle/,
 reference-stream RNG, 64x64 tile queue) timed on this box's cores over a
 bounded sample of the same workload.
 """
@@ -33,6 +41,10 @@ import json
 import os
 import sys
 import time
+
+# dmabuf IPC for RCCL and cross-process CUDA tensors (the host driver has no legacy IPC); it must be in
+# the environment before torch (and HIP) initialise
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 METRIC = "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU scaling"
@@ -175,6 +187,9 @@ def main():
                          "after one warm-up frame, same ranks and sharding (0 = skip)")
     ap.add_argument("--dump-frame", default="",
                     help="rank 0 saves the accumulated frame of the last timed step (.npy; tests)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the distributed path (process group, the framebuffer reduce into rank 0, the "
+                         "all-reduces of the totals) even with one rank, e.g. RCCL at --nproc-per-node 1")
     args = ap.parse_args()
 
     import torch
@@ -183,11 +198,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    distributed = world > 1
+    distributed = world > 1 or args.force_dist
     # one GPU per rank; ranks beyond the visible GPUs share them (gloo tests on a 1-GPU box)
     device = local_rank % max(1, torch.cuda.device_count())
     if distributed:
-        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(device)
         dist.init_process_group(args.dist_backend, rank=rank, world_size=world)
     torch.cuda.set_device(device)
@@ -218,7 +232,7 @@ def main():
         # per-scene settings (rt_scene_config): this scene's shard mode, pool and environment NEE
         dev.configure(shard_mode=shard_mode, path_pool=args.pool, env_sampling=1 if args.env_sampling else 0)
         accum = torch.zeros((fh, fw, 4), dtype=torch.float32, device=f"cuda:{device}")
-        scratch = torch.zeros_like(accum) if world > 1 else None
+        scratch = torch.zeros_like(accum) if distributed else None
 
         def render_shard(shard_index, shard_count, buf):
             return dev.render_device(cam, st, fc, fw, fh, buf.data_ptr(), stream=stream.cuda_stream,
@@ -230,7 +244,7 @@ def main():
                 return render_shard(args.shard_index, args.shard_of, accum)
             # this rank's share into a zeroed frame buffer, the RCCL sum-reduce of it over xGMI into
             # rank 0, which adds it to its accumulation buffer
-            return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch)
+            return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch, reduce=distributed)
         return scene, dev, st, post, accum, step
 
     scene, dev, st, post, accum, step = setup(args.config, w, h, asset_dir)
@@ -258,6 +272,8 @@ def main():
     if os.environ.get("RT_BENCH_NO_STAGE_EVENTS"):
         rt.lib().rt_set_profiling(0)
     closest = shadow = samples = traced = traced_sh = 0
+    steps_k = [0, 0]                 # trace steps (rt_stats::trace_steps) of the timed frames, per kind
+    trav = [dict.fromkeys(rt.abi.TRAVERSAL_FIELDS, 0) for _ in range(2)]
     kms = [0.0] * 6
     kl = [0] * 6
     if distributed:
@@ -271,6 +287,10 @@ def main():
         samples += s.samples
         traced += s.traced_rays[0]
         traced_sh += s.traced_rays[1]
+        for k in range(2):
+            steps_k[k] += s.trace_steps[k]
+            for f in rt.abi.TRAVERSAL_FIELDS:
+                trav[k][f] += getattr(s.traversal[k], f)
         for k in range(6):
             kms[k] += s.kernel_ms[k]
             kl[k] += s.kernel_launches[k]
@@ -280,12 +300,17 @@ def main():
     elapsed = time.perf_counter() - t0
     rt.lib().rt_set_profiling(0)
 
-    totals = torch.tensor([closest, shadow, samples, traced, traced_sh], dtype=torch.float64, device=red_dev)
+    totals = torch.tensor([closest, shadow, samples, traced, traced_sh] + steps_k +
+                          [trav[k][f] for k in range(2) for f in rt.abi.TRAVERSAL_FIELDS],
+                          dtype=torch.float64, device=red_dev)
     tmax = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
     if distributed:
         dist.all_reduce(totals, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    closest_all, shadow_all, samples_all, traced_all, traced_sh_all = [float(x) for x in totals.tolist()]
+    tl = [float(x) for x in totals.tolist()]
+    closest_all, shadow_all, samples_all, traced_all, traced_sh_all = tl[:5]
+    nf = len(rt.abi.TRAVERSAL_FIELDS)
+    trav_all = [{f: int(tl[7 + k*nf + i]) for i, f in enumerate(rt.abi.TRAVERSAL_FIELDS)} for k in range(2)]
     elapsed = float(tmax.item())
     if args.dump_frame and rank == 0:
         import numpy as np
@@ -357,33 +382,30 @@ def main():
                             "frac": round(iso_gbs / HBM_PEAK_GBS, 4), "source": tj.get("source")}
         except (OSError, ValueError, KeyError):
             pass
-        # Traversal kernels are bound by dependent L2 / Infinity Cache fetches, not HBM: their
-        # second figure is the bytes the steps fetch (steps per ray from profiles/step_stats.json, an
-        # RT_STEP_STATS build, x 128 B) over the launches' HIP-event time in the warm-up frames (every
-        # stage timed there), against the L2 gather rate (MI355X_MICROARCH.md, rows shared by every
-        # workgroup: 16.8-18.8 TB/s).  Reported for both trace kernels whichever kernel dominates.
+        # Traversal kernels are bound by dependent L2 / Infinity Cache fetches, not HBM: their second
+        # figure is the bytes their steps fetch -- every step loads one 128-byte round per lane (a BVH4
+        # node, two triangles or a leaf record) -- counted in the timed frames by the kernels themselves
+        # (rt_stats::trace_steps, rank 0), over the launches' HIP-event time in the warm-up frames (every
+        # stage timed there; the frames are identical), against the L2 gather rate (MI355X_MICROARCH.md,
+        # rows shared by every workgroup: 16.8-18.8 TB/s).  Reported for both trace kernels.
         traversal = None
-        try:
-            with open(os.path.join(ROOT, "profiles", "step_stats.json")) as f:
-                sj = json.load(f)
-            per_cfg = sj.get("configs", {}).get(args.config)
-            if per_cfg and args.warmup:
-                traversal = {"peak": L2_PEAK_GBS, "unit": "GB/s", "source": sj.get("source"),
-                             "timing": "warm-up frames, HIP events on each partition's stream (shared GPU)"}
-                for stage, kname, rays in (("extend", "k_extend", wtraced[0]), ("connect", "k_connect", wtraced[1])):
-                    ent = per_cfg.get(kname)
-                    k = STAGES.index(stage)
-                    if not ent or not wl[k] or wms[k] <= 0:
-                        continue
-                    per_launch = rays / wl[k]
-                    tb = ent["steps_per_ray"] * sj["bytes_per_step"] * per_launch
-                    mean_s = wms[k] * args.warmup / wl[k] / 1e3
-                    t_gbs = tb / mean_s / 1e9
-                    traversal[kname] = {"rays_per_launch": round(per_launch), "steps_per_ray": ent["steps_per_ray"],
-                                        "bytes_per_launch": round(tb), "mean_launch_ms": round(mean_s * 1e3, 4),
-                                        "achieved": round(t_gbs, 1), "frac": round(t_gbs / L2_PEAK_GBS, 4)}
-        except (OSError, ValueError, KeyError):
-            pass
+        if args.warmup:
+            traversal = {"peak": L2_PEAK_GBS, "unit": "GB/s", "bytes_per_step": 128,
+                         "source": "rt_stats::trace_steps of the timed frames (counted on the device)",
+                         "timing": "warm-up frames, HIP events on each partition's stream (shared GPU)"}
+            for kind, (stage, kname, rays) in enumerate((("extend", "k_extend", traced), ("connect", "k_connect", traced_sh))):
+                k = STAGES.index(stage)
+                if not wl[k] or wms[k] <= 0 or not rays:
+                    continue
+                launches = wl[k] / args.warmup                     # per frame
+                steps = steps_k[kind] / args.steps                  # per frame
+                tb = 128.0 * steps / launches
+                mean_s = wms[k] / launches / 1e3
+                t_gbs = tb / mean_s / 1e9
+                traversal[kname] = {"rays_per_launch": round(rays / args.steps / launches),
+                                    "steps_per_ray": round(steps_k[kind] / rays, 3),
+                                    "bytes_per_launch": round(tb), "mean_launch_ms": round(mean_s * 1e3, 4),
+                                    "achieved": round(t_gbs, 1), "frac": round(t_gbs / L2_PEAK_GBS, 4)}
         ref = wms if args.warmup else [x / args.steps for x in kms]        # all stages: warm-up frames
         concurrency = sum(ref[:5]) / (elapsed * 1e3 / args.steps) if elapsed > 0 else 0.0
         pipe_bytes = PIPE_BYTES_PER_RAY * (closest + shadow) + PIPE_BYTES_PER_SAMPLE * samples
@@ -413,7 +435,7 @@ def main():
             cpu = cpu_baseline(rt, cfg, args.spp, args.cpu_seconds)
         parallelism = (f"{args.shard_mode}%{args.shard_of} (rank {args.shard_index} only, diagnostic)"
                        if args.shard_of > 1 else f"{args.shard_mode}%{world}" +
-                       (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_reduce" if world > 1 else ""))
+                       (f"+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}_reduce" if distributed else ""))
         out = {
             "metric": METRIC,
             "value": round(mrays, 3),
@@ -457,6 +479,12 @@ def main():
                                   enumerate(STAGES)},
             "stage_ms_note": ("HIP-event time per stage summed over its launches, from the warm-up frames "
                               "(4 partitions overlap, so the sum exceeds ms_per_step)"),
+            # the reference's per-frame TraversalStats (RT/intersection.h:33-40), counted on the device in
+            # this library's walk and BVH4 units (include/rt_abi.h), per frame, all ranks
+            "traversal_stats": {"per_frame": {f: (trav_all[0][f] + trav_all[1][f]) // args.steps
+                                              for f in rt.abi.TRAVERSAL_FIELDS},
+                                "closest": {f: v // args.steps for f, v in trav_all[0].items()},
+                                "shadow": {f: v // args.steps for f, v in trav_all[1].items()}},
             "c4": c4,
             "cpu_baseline": cpu,
             "postprocess": postprocess,

@@ -218,7 +218,9 @@ def load_preset(name, w, h, asset_dir=None):
     ok = lib().rth_load_preset(name.encode(), w, h, asset_dir.encode() if asset_dir else None, C.byref(handle),
                                C.byref(cam), C.byref(st), C.byref(fc), C.byref(post))
     if not ok:
-        raise ValueError(f"unknown preset {name!r}")
+        why = lib().rth_last_error()
+        why = why.decode() if isinstance(why, bytes) else why
+        raise ValueError(f"preset {name!r}: " + (why or "unknown preset"))
     return Scene(handle.value), cam, st, fc, post
 
 

@@ -122,18 +122,35 @@ class TileSet(C.Structure):
     _fields_ = [("tile_w", C.c_uint32), ("tile_h", C.c_uint32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32)]
 
 
+TRAVERSAL_FIELDS = ("mesh_intersection_count", "mesh_bvh_traversals", "mesh_node_traversals", "mesh_leaf_traversals")
+
+
+class TraversalStats(C.Structure):    # TraversalStats RT/intersection.h:33-40 (rt_traversal_stats)
+    _fields_ = [(f, C.c_uint64) for f in TRAVERSAL_FIELDS]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f in TRAVERSAL_FIELDS}
+
+
 class Stats(C.Structure):
     _fields_ = [("closest_hit_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
                 ("iterations", C.c_uint64), ("seconds", C.c_double),
                 ("kernel_ms", C.c_double * RT_KERNEL_COUNT), ("kernel_launches", C.c_uint64 * RT_KERNEL_COUNT),
-                ("traced_rays", C.c_uint64 * 2), ("splat_mode", C.c_int32), ("reserved", C.c_int32)]
+                ("traced_rays", C.c_uint64 * 2), ("splat_mode", C.c_int32), ("reserved", C.c_int32),
+                ("traversal", TraversalStats * 2), ("trace_steps", C.c_uint64 * 2)]
+
+    def traversal_total(self):
+        """The reference's TraversalStats: both query kinds summed."""
+        return {f: getattr(self.traversal[0], f) + getattr(self.traversal[1], f) for f in TRAVERSAL_FIELDS}
 
     def as_dict(self):
         return {"closest_hit_rays": self.closest_hit_rays, "shadow_rays": self.shadow_rays,
                 "samples": self.samples, "iterations": self.iterations, "seconds": self.seconds,
                 "kernel_ms": {RT_KERNEL_NAMES[i]: self.kernel_ms[i] for i in range(6)},
                 "kernel_launches": {RT_KERNEL_NAMES[i]: self.kernel_launches[i] for i in range(6)},
-                "traced_rays": [self.traced_rays[0], self.traced_rays[1]], "splat_mode": self.splat_mode}
+                "traced_rays": [self.traced_rays[0], self.traced_rays[1]], "splat_mode": self.splat_mode,
+                "traversal": [self.traversal[0].as_dict(), self.traversal[1].as_dict()],
+                "trace_steps": [self.trace_steps[0], self.trace_steps[1]]}
 
 
 class RayQuery(C.Structure):

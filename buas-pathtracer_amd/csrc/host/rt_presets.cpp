@@ -63,6 +63,7 @@ struct Ctx {
     rth_post_settings* post;
     uint32_t w, h;
     std::string asset_dir;
+    bool failed = false;             // a mesh or BVH build failed (rth_last_error says why)
 };
 
 bool exists(const std::string& p) { struct stat st; return stat(p.c_str(), &st) == 0; }
@@ -91,7 +92,9 @@ uint32_t load_mesh(Ctx& c, uint32_t triangles, uint32_t seed) {
     uint32_t n = rth_generate_mesh(triangles, seed, nullptr, nullptr);
     std::vector<rt_v3> t(3*(size_t)n), nn(3*(size_t)n);
     rth_generate_mesh(triangles, seed, t.data(), nn.data());
-    return rth_create_mesh(c.s, n, t.data(), nn.data(), RTH_BVH_SAH_BINNED);
+    const uint32_t id = rth_create_mesh(c.s, n, t.data(), nn.data(), RTH_BVH_SAH_BINNED);
+    if (id == 0xFFFFFFFFu) c.failed = true;      // e.g. out of memory in the BVH build
+    return id;
 }
 
 // load_environment_map with the synthetic stand-in for the missing 2k .hdr files.
@@ -434,10 +437,12 @@ extern "C" int rth_load_preset(const char* name_c, uint32_t w, uint32_t h, const
     else if (name == "c5") { dragon(c, 62500, true, 3, true); st->samples_per_pixel = 1024;
                              st->sampling_strategy = RT_SAMPLING_OPTIMIZED_BLUE_NOISE; }
     else ok = false;
-    if (!ok) { rth_scene_destroy(s); return 0; }
+    // a failed mesh or scene BVH build fails the preset (rth_last_error says why) instead of leaving an
+    // out-of-range mesh id or no top level in the scene
+    if (!ok || c.failed) { rth_scene_destroy(s); return 0; }
     st->integrator = RT_INTEGRATOR_ADVANCED;   // the hot path is the Advanced Pathtracer
     rth_recompute_camera(cam);                 // render_all_tiles -> recompute_camera (:717)
-    rth_create_scene_bvh(s);                   // load_scene (:1465)
+    if (!rth_create_scene_bvh(s)) { rth_scene_destroy(s); return 0; }   // load_scene (:1465)
     *out_scene = s;
     return 1;
 }

@@ -45,12 +45,10 @@ RT_D V3 neg(V3 a) { return {-a.x, -a.y, -a.z}; }
 // neither the residual nor the result leaves the normal range.  Other inputs (zeros,
 // denormals, huge values, inf, NaN) take the full division; a wave whose lanes are all
 // in range skips it.  rt_debug_verify_rcp checks it against the IEEE division for
-// every one of the 2^32 floats (tests/test_gpu_parity.py::test_rcp_cr_exhaustive).
-#ifndef RT_RCP_CR
-#define RT_RCP_CR 1
-#endif
+// every one of the 2^32 floats (tests/test_gpu_parity.py::test_rcp_cr_exhaustive).  The host
+// build of tools/check_sincos.cpp has no v_rcp_f32 and divides (the same bits).
 RT_D float rcp_cr(float x) {
-#if RT_RCP_CR
+#ifndef RT_DMATH_HOST_TEST
     const float a = __builtin_fabsf(x);
     if (a >= 0x1p-125f && a <= 0x1p125f) {
         const float r = __builtin_amdgcn_rcpf(x);

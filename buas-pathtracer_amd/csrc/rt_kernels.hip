@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <mutex>
+#include <cerrno>
 
 #include "rt_dmath.h"
 
@@ -93,28 +94,20 @@ struct DevScene {
     V3 top_sky, bot_sky;
     const uint8_t* strata;          // g_strata_permutation_sets [256][64]
     const uint8_t* bluenoise;       // sobol | scrambling | ranking
-    // The small tables above (materials, primitives, planes, transforms, lights,
-    // top-level sequence and records, meshes, strata) packed into one blob that the
-    // slot-ordered kernels copy into LDS at start (scene_in_lds); 0 = too large.
+    // The small tables above (materials, primitives, planes, transforms, lights, meshes)
+    // packed into one blob that k_shade copies into LDS at start (scene_in_lds); 0 = too large.
     const float4* blob;
     uint32_t blob_q;                // float4 count (<= LDS_SCENE_Q)
-    uint32_t off[10];               // byte offsets of the tables in the blob (BLOB_*)
+    uint32_t off[7];                // byte offsets of the tables in the blob (BLOB_*)
 };
 // The 16 KB strata table is read at bounce 0 only (a few lookups per path): copying
-// it into every block's LDS costs more than the L2 reads it saves
-#ifndef RT_LDS_STRATA
-#define RT_LDS_STRATA 0
-#endif
-// RT_PROLOGUE_SCALAR (default): the ray prologue's tables (top-level sequence, leaf
-// records) stay in HBM -- scene_in_lds does not rebase them -- and its wave-uniform
-// walk reads them with s_load through the scalar cache: no LDS round trip and no
-// readfirstlane per value.  ld_uniform's scalar load needs a global address.
-#ifndef RT_PROLOGUE_SCALAR
-#define RT_PROLOGUE_SCALAR 1
-#endif
+// it into every block's LDS costs more than the L2 reads it saves, so it stays in HBM.
+// The ray prologue's tables (top-level sequence, leaf records) stay in HBM too --
+// scene_in_lds does not rebase them -- and its wave-uniform walk reads them with s_load
+// through the scalar cache: no LDS round trip and no readfirstlane per value
+// (ld_uniform's scalar load needs a global address).
 static_assert(sizeof(rt_primitive) == 32 && offsetof(rt_primitive, p) == 16, "the prologue loads a plane's p[] as one float4");
-enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_TOP_SEQ, BLOB_LEAF_REC,
-       BLOB_MESHES, BLOB_STRATA, BLOB_COUNT };
+enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_MESHES, BLOB_COUNT };
 constexpr uint32_t LDS_SCENE_Q = 2048;   // 32 KB
 // The copy is the launch's dynamic LDS, sized to the blob (blob_q float4): a fixed
 // 32 KB array held 256-thread blocks to 5 per CU whatever the scene's size.
@@ -140,14 +133,7 @@ RT_D DevScene scene_in_lds(const DevScene& sc, float4* lds) {
     s.inv = reinterpret_cast<const M34*>(b + sc.off[BLOB_INV]);
     s.fwd = reinterpret_cast<const M34*>(b + sc.off[BLOB_FWD]);
     s.lights = reinterpret_cast<const uint32_t*>(b + sc.off[BLOB_LIGHTS]);
-#if !RT_PROLOGUE_SCALAR
-    if (sc.top_seq) s.top_seq = reinterpret_cast<const float4*>(b + sc.off[BLOB_TOP_SEQ]);
-    s.leaf_rec = reinterpret_cast<const float4*>(b + sc.off[BLOB_LEAF_REC]);
-#endif
     s.meshes = reinterpret_cast<const DevMesh*>(b + sc.off[BLOB_MESHES]);
-#if RT_LDS_STRATA
-    s.strata = reinterpret_cast<const uint8_t*>(b + sc.off[BLOB_STRATA]);
-#endif
     return s;
 }
 
@@ -375,13 +361,7 @@ RT_D void object_ray(float4 q0, float4 q1, float4 q2, bool translate, bool plain
 // the reference's node_stack[64] (:261, :445).
 // ----------------------------------------------------------------------
 constexpr int STACK_DEPTH = 64;
-#ifndef RT_STACK_LDS
-#define RT_STACK_LDS 16
-#endif
-#ifndef RT_TRI_BATCH
-#define RT_TRI_BATCH 2
-#endif
-constexpr int STACK_LDS = RT_STACK_LDS;
+constexpr int STACK_LDS = 16;
 
 struct Hit {
     float t;
@@ -414,7 +394,7 @@ enum { TM_TOP = 0, TM_LEAF = 1, TM_MESH = 2, TM_DONE = 3 };
 // does next (a sibling pair of nodes, up to TRI_FETCH triangles of a leaf, or a
 // top-level leaf record), then the arithmetic.  Lanes doing different kinds of
 // work in the same step therefore share one memory latency.
-constexpr uint32_t TRI_FETCH = RT_TRI_BATCH;
+constexpr uint32_t TRI_FETCH = 2;
 // Mesh BVHs are traversed as BVH4: each interior node of the caller's BVH2 is
 // merged with its interior children (built at upload, build_bvh4).  A node holds
 // up to 4 children in SoA form, one 128-byte line:
@@ -425,11 +405,8 @@ constexpr uint32_t TRI_FETCH = RT_TRI_BATCH;
 // front-to-back order by d_is_negative, RT/intersection.cpp:328-340); the BVH2
 // level in between is skipped, i.e. its box test, which only culls what its
 // children's own tests cull (their boxes lie inside it).  Halves the interior steps.
-#ifndef RT_MESH_BVH4
-#define RT_MESH_BVH4 1
-#endif
 constexpr uint32_t EMPTY4 = 0xFFFFFFFFu;
-constexpr int FETCH_Q = (RT_MESH_BVH4 ? 8 : (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u));   // float4 per lane per step
+constexpr int FETCH_Q = 8;                       // float4 per lane per step: one 128-byte BVH4 node
 
 // The part of intersect_scene_internal (RT/intersection.cpp:411-598) that needs
 // no BVH: the planes, brute force (:424-433), then the top-level root, which the
@@ -451,10 +428,9 @@ constexpr int FETCH_Q = (RT_MESH_BVH4 ? 8 : (3*TRI_FETCH > 6u ? 3*TRI_FETCH : 6u
 // ray is queued with MLIST_FULL and the kernel re-walks the whole top level
 // (re-testing an analytic primitive at equal t changes nothing: strict tests).
 constexpr uint32_t MLIST_MAX = 4;
-// a load whose address is the same in every active lane, its value moved to SGPRs
-// (RT_PROLOGUE_SCALAR: an s_load through the scalar cache)
+// a load whose address is the same in every active lane: an s_load through the scalar
+// cache, its value in SGPRs
 RT_D float4 ld_uniform(const float4* p) {
-#if RT_PROLOGUE_SCALAR
     // an LDS address here would be a bug (scene_in_lds rebased the table); trap rather
     // than read a wild global address
 #ifdef __HIP_DEVICE_COMPILE__
@@ -465,29 +441,22 @@ RT_D float4 ld_uniform(const float4* p) {
                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
     const __attribute__((address_space(4))) float* f = reinterpret_cast<const __attribute__((address_space(4))) float*>(u);
     return make_float4(f[0], f[1], f[2], f[3]);
-#else
-    const float4 v = *p;
-    return make_float4(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.x))),
-                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.y))),
-                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.z))),
-                       __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v.w))));
-#endif
 }
 constexpr uint32_t MLIST_FULL = 0xFFFFFFFFu;
-struct Prologue { float t; uint32_t code; bool occluded, bvh; V3 inv_d; uint32_t mlist; };
+// calls: the mesh instances the walk reaches -- the top-level leaf holding one passes its pop-time
+// test, it is not the ignored light, and no plane, sphere or box has occluded a shadow query before
+// it: the reference's intersect_mesh calls (RT/intersection.cpp:488, counted at :254) in this walk's
+// order (rt_stats::traversal)
+struct Prologue { float t; uint32_t code; bool occluded, bvh; V3 inv_d; uint32_t mlist, calls; };
 RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ, uint32_t ignored) {
     Prologue r;
     Ray wr = make_ray(o, d, max_t);
     wr.zero = 0u;                                                  // no pruning on the world ray
     r.t = max_t; r.code = RT_HIT_MISS; r.occluded = false; r.bvh = false; r.inv_d = wr.inv_d; r.mlist = MLIST_FULL;
+    r.calls = 0;
     for (uint32_t i = 0; i < sc.plane_count; ++i) {
-#if RT_PROLOGUE_SCALAR
         const float4 pl = ld_uniform(reinterpret_cast<const float4*>(sc.planes_g + i) + 1);   // p[0..3]
         if (ray_plane(wr, {pl.x, pl.y, pl.z}, pl.w, r.t)) {
-#else
-        const rt_primitive& pl = sc.planes[i];
-        if (ray_plane(wr, {pl.p[0], pl.p[1], pl.p[2]}, pl.p[3], r.t)) {
-#endif
             r.code = RT_HIT_PLANE_BIT | i;
             if (occ) { r.occluded = true; return r; }
         }
@@ -500,17 +469,13 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
         r.bvh = bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn) && tn < r.t;
         return r;
     }
-#ifndef RT_PROLOGUE_UNIFORM
-#define RT_PROLOGUE_UNIFORM 1
-#endif
-#if RT_PROLOGUE_UNIFORM
     // Wave-uniform walk: every lane follows octant 0's sequence, so entry and record
     // addresses are the same across the wave (one cache line per load, values moved to
     // SGPRs) and the lanes stay converged; each lane tests only the entries on its own
     // path (`next`).  Octant 0's order differs from the reference's front-to-back order
     // only in which of two surfaces at exactly equal t is kept (see above).
     const float4* seq = sc.top_seq;
-    uint32_t list = 0, n = 0, next = 0;
+    uint32_t list = 0, n = 0, next = 0;     // n: listed instances (bits 0-7) | instances reached << 8
     bool full = false;
     const uint32_t len = sc.top_seq_len;
     const bool plain = plain_ray(o, d);
@@ -542,8 +507,10 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
                 if (type == RT_PRIMITIVE_MESH) {                   // the mesh root's pop-time test (:269-275)
                     const float4 q4 = ld_uniform(q + 4), q5 = ld_uniform(q + 5);
                     float tm;
+                    n += 1u << 8;                                  // intersect_mesh called (:488)
                     if (bv_static(ir, {q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z}, tm) && tm < r.t) {
-                        if (n < sc.mlist_max) list |= j << (6*n);
+                        const uint32_t k = n & 0xFFu;
+                        if (k < sc.mlist_max) list |= j << (6*k);
                         else full = true;
                         ++n;
                     }
@@ -557,54 +524,48 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
             }
         }
     }
+    r.calls = n >> 8;
     if (r.occluded) return r;
-#else
-    const float4* seq = sc.top_seq + 2*(size_t)sc.top_seq_len*(wr.neg & 7u);
-    uint32_t list = 0, n = 0;
-    bool full = false;
-    for (uint32_t i = 0; i < sc.top_seq_len;) {
-        const float4 a = seq[2*i], b = seq[2*i + 1];
-        float tn;
-        const bool pass = bv_static(wr, {a.x, a.y, a.z}, {a.w, b.x, b.y}, tn) && tn < r.t;
-        const uint32_t info = __float_as_uint(b.z), skip = __float_as_uint(b.w);
-        if (!pass || !(info >> 31)) { i = pass ? i + 1 : skip; continue; }
-        const uint32_t first = info & 0xFFFFFFu, end = first + ((info >> 24) & 127u);
-        for (uint32_t j = first; j < end; ++j) {                   // the leaf's primitives in order
-            const float4* q = sc.leaf_rec + (size_t)j*LEAF_REC_Q;
-            const float4 q3 = q[3];
-            const uint32_t pi = __float_as_uint(q3.x), type = __float_as_uint(q3.y) & 0xFFu;
-            if (pi == ignored) continue;
-            M34 inv;
-            const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-            inv.e[0][0] = q0.x; inv.e[0][1] = q0.y; inv.e[0][2] = q0.z; inv.e[0][3] = q0.w;
-            inv.e[1][0] = q1.x; inv.e[1][1] = q1.y; inv.e[1][2] = q1.z; inv.e[1][3] = q1.w;
-            inv.e[2][0] = q2.x; inv.e[2][1] = q2.y; inv.e[2][2] = q2.z; inv.e[2][3] = q2.w;
-            const Ray ir = make_ray(xform(inv, o, 1.0f), xform(inv, d, 0.0f), 0.0f);   // transform_ray :403-409
-            if (type == RT_PRIMITIVE_MESH) {                       // the mesh root's pop-time test (:269-275)
-                const float4 q4 = q[4], q5 = q[5];
-                float tm;
-                if (bv_static(ir, {q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z}, tm) && tm < r.t) {
-                    if (n < sc.mlist_max) list |= j << (6*n);
-                    else full = true;
-                    ++n;
-                }
-                continue;
-            }
-            bool hit = false;
-            if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, q3.z, r.t);
-            else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {q3.z, q3.w, q[4].x}, r.t);
-            if (hit) {
-                r.code = pi;
-                if (occ) { r.occluded = true; return r; }
-            }
-        }
-        i = skip;
-    }
-#endif
+    n &= 0xFFu;
     r.bvh = n > 0;
     r.mlist = full ? MLIST_FULL : (list | (n << 24));
     return r;
 }
+
+// What the traversal steps fetched, for the TraversalStats counts (rt_stats::traversal): each
+// step adds one of these to its lane's Traversal::acc, 4-bit count fields.  ST_ENTRY a mesh
+// instance's top-level leaf record (its object-space ray and root box test: intersect_mesh
+// entered); ST_NODE a mesh BVH4 interior node; ST_LEAF the first triangles of a mesh leaf (the
+// leaf entered); ST_TRIS any step that fetched triangles; ST_TOP a top-level interior node or a
+// sphere's / box's record.  A lane's fields stay below 16 between two flushes (StepCounts).
+constexpr uint32_t ST_ENTRY = 1u << 0, ST_NODE = 1u << 4, ST_LEAF = 1u << 8, ST_TRIS = 1u << 12, ST_TOP = 1u << 16;
+
+// TraversalStats counters of a partition: per ray kind (0 closest, 1 shadow) and shard, TV_* counts.
+enum { TV_ENTRIES, TV_NODES, TV_LEAVES, TV_TRIS, TV_TOP, TV_CALLS, TV_N = 8 };
+extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
+// A wave's step counts.  flush, at a point every lane of the wave reaches, sums the lanes' `acc`
+// (taken from Traversal::acc: 4-bit fields, at most 15 steps per lane since the last flush) over the
+// wave with DPP reductions into the wave's totals, which stay in SGPRs; commit: one lane adds the
+// totals to the partition's counters.
+template <bool LST>
+struct StepCounts {
+    uint32_t acc = 0;
+    uint32_t tot[5] = {0, 0, 0, 0, 0};                 // TV_ENTRIES .. TV_TOP
+    RT_D void flush() {
+        const uint32_t a = __ockl_wfred_add_u32((acc & 0xFu) | ((acc & 0xF0u) << 12));          // entries | nodes
+        const uint32_t b = __ockl_wfred_add_u32(((acc >> 8) & 0xFu) | ((acc & 0xF000u) << 4));  // leaves | tris
+        tot[TV_ENTRIES] += a & 0xFFFFu; tot[TV_NODES] += a >> 16;
+        tot[TV_LEAVES] += b & 0xFFFFu; tot[TV_TRIS] += b >> 16;
+        if (!LST) tot[TV_TOP] += __ockl_wfred_add_u32((acc >> 16) & 0xFu);
+        acc = 0;
+    }
+    RT_D void commit(unsigned long long* trav, int kind) const {
+        if (__lane_id() != (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) return;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (tot[i]) atomicAdd(&trav[kind*TV_N + i], (unsigned long long)tot[i]);
+    }
+};
 
 template <bool OCC, bool LST = false>
 struct Traversal {
@@ -624,12 +585,6 @@ struct Traversal {
     uint32_t inst, node_off, tri_off;   // TM_MESH: the instance
     uint32_t cur_lf, cur_cnt, cur_ax;   // node held by the lane (cur_cnt: leaf size, 0 interior)
     bool has_cur, occluded, finite_world;
-#ifdef RT_STEP_STATS
-    uint32_t stat[8] = {};              // lane steps, wave steps*64, pops, -, interior, leaf, record, rays
-#define RT_STAT(i) (++stat[i])
-#else
-#define RT_STAT(i) ((void)0)
-#endif
 
     RT_D Ray cur_ray() const {
         Ray r; r.o = co; r.d = cd; r.inv_d = cinv; r.neg = cflags & 7u; r.zero = cflags >> 3; r.max_t = 0.0f;
@@ -712,7 +667,6 @@ struct Traversal {
     RT_D bool pop(const Stack& st, const rt_bvh_node* nodes, int base) {
         while (sp > base) {
             const uint2 e = st.get<SH>(--sp);
-            RT_STAT(2);
             if (__uint_as_float(e.y) < t) {
                 unpack_node(nodes, e.x, cur_lf, cur_cnt, cur_ax);
                 has_cur = true;
@@ -750,24 +704,27 @@ struct Traversal {
         }
     }
 
-    // One traversal step; returns false once the query is finished (mode == TM_DONE).
+    // One traversal step; returns false once the query is finished (mode == TM_DONE).  What the
+    // step fetched is added to `acc` (ST_*, the lane's TraversalStats counts since the last flush).
     // A step pops before it pushes and pushes at most PUSH_MAX entries, so when no lane of
     // the wave is within PUSH_MAX levels of STACK_LDS the whole step stays in LDS.
-    static constexpr int PUSH_MAX = RT_MESH_BVH4 ? 4 : 2;
+    static constexpr int PUSH_MAX = 4;
+    uint32_t acc = 0;                   // ST_* fields of the steps since the caller last took them
     RT_D bool step(const DevScene& sc, const Stack& st) {
         if (__ballot(sp > STACK_LDS - PUSH_MAX || !(cflags & 64u)) == 0ull) return step_impl<true, true>(sc, st);
         return step_impl<false, false>(sc, st);
     }
     template <bool SH, bool FIN>
     RT_D bool step_impl(const DevScene& sc, const Stack& st) {
-        RT_STAT(0);
         // 1. state changes that need no global memory
-        if (mode == TM_MESH && !has_cur && !pop<SH>(st, sc.mnodes_src + node_off, mesh_base)) {
+        const bool take = mode == TM_MESH && !has_cur;
+        if (take && !pop<SH>(st, sc.mnodes_src + node_off, mesh_base)) {
             mode = TM_LEAF;                                        // instance finished
             set_world();
         }
+        const bool fresh = take && mode == TM_MESH;               // a mesh node popped in this step
         if (mode == TM_LEAF && leaf_cur == leaf_end) {
-            if (LST) { mode = TM_DONE; return false; }             // the mesh list is the whole walk
+            if (LST) { mode = TM_DONE; return false; }           // the mesh list is the whole walk
             mode = TM_TOP;
         }
         if (!LST && mode == TM_TOP) {
@@ -781,18 +738,12 @@ struct Traversal {
         const float4* src;
         uint32_t nq;
         if (mode == TM_LEAF) {
-            RT_STAT(6);
             src = sc.leaf_rec + (size_t)((LST || listed) ? (leaf_list & 63u) : leaf_cur)*LEAF_REC_Q; nq = LEAF_REC_Q;
         } else if (cur_cnt) {                                      // mesh leaf
-            RT_STAT(5);
             src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
         } else {                                                   // interior: the sibling pair
-            RT_STAT(4);
-#if RT_MESH_BVH4
             if (LST || mode == TM_MESH) { src = sc.mnodes4 + 8*(size_t)cur_lf; nq = 8; }
-            else
-#endif
-            { src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4; }
+            else { src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4; }
         }
         // unconditional: every array the step reads is padded by FETCH_Q float4 at upload
         (void)nq;
@@ -803,7 +754,7 @@ struct Traversal {
         if (mode == TM_LEAF) {
             const uint32_t pi = __float_as_uint(F[3].x);
             ++leaf_cur; leaf_list >>= 6;
-            if (pi == ignored) return true;
+            if (pi == ignored) { acc += ST_TOP; return true; }
             const uint32_t type = __float_as_uint(F[3].y) & 0xFFu;
             M34 inv;
             inv.e[0][0] = F[0].x; inv.e[0][1] = F[0].y; inv.e[0][2] = F[0].z; inv.e[0][3] = F[0].w;
@@ -820,6 +771,7 @@ struct Traversal {
                 float tn;
                 if (bv_static(ir, rp, rr, tn)) push<SH>(st, __float_as_uint(F[4].x), tn);
                 mode = TM_MESH;
+                acc += ST_ENTRY;
                 return true;
             }
             if (!LST) {
@@ -827,13 +779,15 @@ struct Traversal {
                 if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, F[3].z, t);
                 else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {F[3].z, F[3].w, F[4].x}, t);
                 if (hit) {
-                    if (OCC) { occluded = true; mode = TM_DONE; return false; }
+                    if (OCC) { occluded = true; mode = TM_DONE; acc += ST_TOP; return false; }
                     code = pi;
                 }
             }
+            acc += ST_TOP;
             return true;
         }
         if (cur_cnt) {                                             // mesh leaf: triangles in order
+            acc += fresh ? (ST_LEAF | ST_TRIS) : ST_TRIS;
             Ray r; r.o = co; r.d = cd;
             const uint32_t g0 = tri_off + cur_lf;
 #pragma unroll
@@ -849,12 +803,10 @@ struct Traversal {
             else has_cur = false;
             return true;
         }
-#if RT_MESH_BVH4
-        if (LST || mode == TM_MESH) push_children4<SH, FIN>(st, F);
-        else
-#endif
-        push_children<SH, FIN>(st, F);
         has_cur = false;
+        if (LST || mode == TM_MESH) { push_children4<SH, FIN>(st, F); acc += ST_NODE; return true; }
+        push_children<SH, FIN>(st, F);
+        acc += ST_TOP;
         return true;
     }
 
@@ -971,14 +923,6 @@ RT_D float sample_1d(const DevScene& sc, const SamplerState& s, Rng& rng, int di
 // ======================================================================
 // Integrator helpers (RT/integrators.cpp)
 // ======================================================================
-// d_sincosf in the indirect bounce's hemisphere sample; the NEE light sample keeps the two calls
-// (there the fused form's two live results cost k_shade 8 B of scratch at 64 VGPRs)
-#ifndef RT_SINCOS_NEE
-#define RT_SINCOS_NEE 0
-#endif
-#ifndef RT_SINCOS_IND
-#define RT_SINCOS_IND 1
-#endif
 RT_D V3 random_in_unit_sphere(Rng& e) {                                   // :11-19
     V3 r;
     int guard = 0;   // bounded (a degenerate all-zero RandomSeries would spin forever)
@@ -1000,25 +944,17 @@ RT_D V3 oriented_around_normal(V3 v, V3 n) {                             // :58-
 RT_D V3 map_to_hemisphere(V3 N, V2 rs) {                                 // :93-105
     float az = TAU_32*rs.x, y = rs.y;
     float s = __builtin_sqrtf(1.0f - y*y);
-#if RT_SINCOS_NEE
-    float sa, ca;
-    d_sincosf(az, sa, ca);                          // = d_sinf(az), d_cosf(az), bit for bit
-    V3 h = {ca*s, y, sa*s};
-#else
+    // two calls, not d_sincosf: in the NEE light sample the fused form's two live results cost
+    // k_shade 8 B of scratch at 64 VGPRs
     V3 h = {d_cosf(az)*s, y, d_sinf(az)*s};
-#endif
     return oriented_around_normal(h, N);
 }
 RT_D V3 map_to_cosine_weighted_hemisphere(V3 N, V2 rs) {                 // :107-119
     float az = TAU_32*rs.x, y = rs.y;
     float s = __builtin_sqrtf(1.0f - y);
-#if RT_SINCOS_IND
     float sa, ca;
-    d_sincosf(az, sa, ca);
+    d_sincosf(az, sa, ca);                          // = d_sinf(az), d_cosf(az), bit for bit
     V3 h = {ca*s, __builtin_sqrtf(y), sa*s};
-#else
-    V3 h = {d_cosf(az)*s, __builtin_sqrtf(y), d_sinf(az)*s};
-#endif
     return oriented_around_normal(h, N);
 }
 RT_D float fresnel_dielectric(float ci, float ei, float et, float eta, float& co) {   // :235-258
@@ -1139,19 +1075,12 @@ RT_D uint32_t pick_random_light(const DevScene& sc, const rt_settings& st, float
 // ======================================================================
 // Streaming access to the path pool, the queues and the sample records: each is read
 // or written once per iteration (hundreds of MB per launch, no reuse before the next
-// iteration), so with RT_NT_POOL they use non-temporal loads and stores and do not
-// displace the BVH nodes and triangles the trace kernels keep re-reading from L2.
-#ifndef RT_NT_POOL
-#define RT_NT_POOL 1
-#endif
-#ifndef RT_NT_SPLAT
-#define RT_NT_SPLAT 1
-#endif
+// iteration), so they use non-temporal loads and stores and do not displace the BVH
+// nodes and triangles the trace kernels keep re-reading from L2.
 typedef float nt_f4 __attribute__((ext_vector_type(4)));
 typedef uint32_t nt_u4 __attribute__((ext_vector_type(4)));
 typedef float nt_f2 __attribute__((ext_vector_type(2)));
 typedef uint32_t nt_u2 __attribute__((ext_vector_type(2)));
-#if RT_NT_POOL
 RT_D float4 ldnt(const float4* p) { const nt_f4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f4*>(p)); return make_float4(v.x, v.y, v.z, v.w); }
 RT_D uint4 ldnt(const uint4* p) { const nt_u4 v = __builtin_nontemporal_load(reinterpret_cast<const nt_u4*>(p)); return make_uint4(v.x, v.y, v.z, v.w); }
 RT_D float2 ldnt(const float2* p) { const nt_f2 v = __builtin_nontemporal_load(reinterpret_cast<const nt_f2*>(p)); return make_float2(v.x, v.y); }
@@ -1164,10 +1093,6 @@ RT_D void stnt(float2* p, float2 v) { const nt_f2 t = {v.x, v.y}; __builtin_nont
 RT_D void stnt(float* p, float v) { __builtin_nontemporal_store(v, p); }
 RT_D void stnt(uint2* p, uint2 v) { const nt_u2 t = {v.x, v.y}; __builtin_nontemporal_store(t, reinterpret_cast<nt_u2*>(p)); }
 RT_D void stnt(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
-#else
-template <typename T> RT_D T ldnt(const T* p) { return *p; }
-template <typename T> RT_D void stnt(T* p, T v) { *p = v; }
-#endif
 // The path state is double-buffered: k_shade reads a wave's 64 slots of the current buffer
 // and writes the paths that continue, compacted to the front of the same 64 slots of the
 // other buffer (PathOut), and the paths that end into the finished array; the next
@@ -1199,15 +1124,14 @@ struct Pool {
     uint16_t* mstack;    // [64][n]
     uint8_t*  state;     // S_FREE / S_TRACE / S_DONE / S_NEW (a traced camera ray) per slot
     float4*   ext_rec[2];// extension queues (ping-pong), REC_Q float4 per ray: {o, slot}, {d, t after planes}, {1/d, -}
-    // The shadow queue.  RT_SH_STAGE (default): k_shade writes a queued shadow ray's record and
-    // contribution at its own slot as soon as the ray's prologue is done (so they are not held in
-    // registers across the next bounce's prologue), the queue entry is just that slot, and the
-    // NEE term's destination goes to sh_dst[slot] at the tail.  Otherwise all of it is at the queue
-    // position and sh_slot holds the destination.
-    uint32_t* sh_slot;   // [Q] RT_SH_STAGE: the slot holding the ray; else its destination
-    float4*   sh_rec;    // REC_Q float4 per ray: {o, light id}, {d, max_t}, {1/d, mesh list}
-    float4*   sh_c;      // contribution.xyz
-    uint32_t* sh_dst;    // [N] RT_SH_STAGE: the NEE term's destination (survivor's nx slot or SH_FIN | entry)
+    // The shadow queue.  k_shade writes a queued shadow ray's record and contribution at its own
+    // slot as soon as the ray's prologue is done (so they are not held in registers across the next
+    // bounce's prologue), the queue entry is just that slot, and the NEE term's destination goes to
+    // sh_dst[slot] at the tail.  (k_drain_list reuses sh_slot for its list of live slots.)
+    uint32_t* sh_slot;   // [Q] the slot holding the ray
+    float4*   sh_rec;    // [N] REC_Q float4 per ray: {o, light id}, {d, max_t}, {1/d, mesh list}
+    float4*   sh_c;      // [N] contribution.xyz
+    uint32_t* sh_dst;    // [N] the NEE term's destination (survivor's nx slot or SH_FIN | entry)
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
     uint32_t* free_n;    // [blocks]: the block's slots past its survivors, for the next k_generate (k_shade)
     uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
@@ -1234,43 +1158,16 @@ struct Pool {
 // slot order (thread i = slot i): the SoA loads coalesce, and the queues it
 // appends to come out as runs of consecutive slots (one run per wavefront).
 enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2, S_NEW = 3 };
-// RT_GEN_LEAN (default): k_generate writes a new path as S_NEW without its throughput and
-// total_color records (1, 0 and the bounce-0 flags), and k_shade / k_drain make them from the
-// state, the vignette from the camera ray (new_path_records); 32 B per new path less to write.
-#ifndef RT_GEN_LEAN
-#define RT_GEN_LEAN 1
-#endif
-// k_generate loads its claims and the claimed samples' pixels before it splats (see k_generate)
-#ifndef RT_GEN_HOIST
-#define RT_GEN_HOIST 1
-#endif
-#ifndef RT_GEN_PRIO
-#define RT_GEN_PRIO 0
-#endif
-#ifndef RT_DRAIN_PRIO
-#define RT_DRAIN_PRIO 0
-#endif
+// k_generate writes a new path as S_NEW without its throughput and total_color records (1, 0 and
+// the bounce-0 flags), and k_shade / k_drain make them from the state, the vignette from the camera
+// ray (new_path_records); 32 B per new path less to write.
 constexpr int REC_Q = 3;     // float4 per queued ray record
-#ifndef RT_SH_STAGE
-#define RT_SH_STAGE 1
-#endif
-// k_shade writes a survivor's state before the ray prologues, total_color and the hit record after
-#ifndef RT_SHADE_EARLY
-#define RT_SHADE_EARLY 1
-#endif
-// k_shade keeps the values it only writes out at the end in LDS (needs RT_SHADE_EARLY)
-#ifndef RT_SHADE_STASH
-#define RT_SHADE_STASH RT_SHADE_EARLY
-#endif
 constexpr uint32_t SH_FIN = 0x80000000u;   // Pool::sh_slot: the shadow ray's path is in the finished array
 
 // Queues and fetch heads are sharded NSHARD ways (shard = blockIdx % NSHARD, the
 // blocks that share an XCD), each counter on a 128-B line of its own: one word
 // saturates at ~88 returning atomics/us, and a 2M-slot pool has 4096 blocks.
-#ifndef RT_NSHARD
-#define RT_NSHARD 8
-#endif
-constexpr int NSHARD = RT_NSHARD;
+constexpr int NSHARD = 8;
 static_assert(NSHARD <= 64 && (NSHARD & (NSHARD - 1)) == 0, "k_bookkeep sums the shards in one wave");
 constexpr int NXCD = 8;                        // MI355X: workgroups are dealt round robin over 8 XCDs
 constexpr int LINE_WORDS = 32;
@@ -1292,9 +1189,9 @@ struct Counters {
                                     // path to its end in k_drain; its extend / shade / connect exit
     uint32_t drain_count[NSHARD][LINE_WORDS];   // k_drain_list: live slots per shard (in Pool::sh_slot)
     uint32_t drain_fetch[NSHARD][LINE_WORDS];   // k_drain: items handed out per shard
-    unsigned long long step_stats[2][8];   // RT_STEP_STATS builds: see k_trace
-    uint32_t max_steps[2];          // diagnostics: longest traversal (steps) per kind
-    float    worst_ray[2][8];       // o.xyz, d.xyz, max_t, steps of a ray above the step threshold
+    // TraversalStats of the frame (rt_stats::traversal), per ray kind (0 closest, 1 shadow): TV_* counts,
+    // one 128-byte line per shard (the block's or wave's shard adds to it; the host sums the shards)
+    unsigned long long trav[NSHARD][2*TV_N];
     unsigned long long next_sample;
     unsigned long long total_samples;
     unsigned long long closest_rays;
@@ -1512,10 +1409,7 @@ RT_D uint32_t tile_of(const FrameParams& fp, uint32_t x, uint32_t y) { return di
 // ======================================================================
 // Kernels
 // ======================================================================
-#ifndef RT_BLOCK
-#define RT_BLOCK 256
-#endif
-constexpr int BLOCK = RT_BLOCK;      // slot-ordered kernels (generate / shade)
+constexpr int BLOCK = 256;      // slot-ordered kernels (generate / shade)
 constexpr int EV_SLOTS = 8;     // iterations in flight per partition in run_frame (2 chunks of 4)
 
 // The splat of a finished path (RT/raytracer.cpp:469-488): vignette (L . vig), then the
@@ -1533,13 +1427,8 @@ RT_D void splat_sample(const FrameParams& fp, const Pool& pool, V3 L, float vig,
             // deterministic paths: store the sample; k_resolve_tiles / k_resolve gather it
             const uint32_t rel = key - pool.rec_pass0;
             const size_t rec = (size_t)(rel < pool.rec_ring ? rel : rel % pool.rec_ring)*fp.pixels + p;
-#if RT_NT_SPLAT
             stnt(&pool.rec_rgbx[rec], make_float4(r.x, r.y, r.z, j.x));     // read again only by the resolve
             stnt(&pool.rec_jy[rec], j.y);
-#else
-            pool.rec_rgbx[rec] = make_float4(r.x, r.y, r.z, j.x);
-            pool.rec_jy[rec] = j.y;
-#endif
         } else if (fp.cache_size) {
             const uint32_t xy = fp.pix_xy[p];
             const int64_t x = xy & 0xFFFFu, y = xy >> 16;
@@ -1588,13 +1477,13 @@ __global__ void __launch_bounds__(256) k_pixel_map(FrameParams fp, uint32_t* out
 }
 
 // The vignette of a camera ray (RT/raytracer.cpp:451-453): k_generate stores it with the path, and
-// under RT_GEN_LEAN k_shade / k_drain recompute it from the stored direction (same operations, same bits).
+// k_shade / k_drain recompute it from the stored direction (same operations, same bits).
 RT_D float camera_vignette(const FrameParams& fp, const rt_settings& st, V3 rd) {
     float vig = dot(rd, fp.cz);
     vig = vig*vig*vig*vig;
     return lerpf_(1.0f, vig, st.vignette_strength);
 }
-// The throughput and total_color records of an S_NEW path (RT_GEN_LEAN), as k_generate would have
+// The throughput and total_color records of an S_NEW path, as k_generate would have
 // written them: throughput (1, 1, 1 | vignette), total_color (0, 0, 0 | bounce 0, specular)
 RT_D void new_path_records(const FrameParams& fp, const rt_settings& st, float4 d4, float4& t4, float4& L4) {
     t4 = make_float4(1.0f, 1.0f, 1.0f, camera_vignette(fp, st, ld3(d4)));
@@ -1614,37 +1503,21 @@ RT_D V2 sample_jitter(const DevScene& sc, const rt_settings& st, const FramePara
     return {aa.x - 0.5f, aa.y - 0.5f};
 }
 
-// k_generate reads only the sampler tables and the ray prologue's tables, which stay in HBM
-// (RT_LDS_STRATA = 0) and are read through the scalar cache (RT_PROLOGUE_SCALAR): a block
-// needs no LDS copy of the scene, so it skips that copy, its barrier and its LDS footprint.
-#ifndef RT_GEN_LDS_SCENE
-#define RT_GEN_LDS_SCENE (!RT_PROLOGUE_SCALAR || RT_LDS_STRATA)
-#endif
-constexpr uint32_t GEN_LDS_Q_SCALE = RT_GEN_LDS_SCENE ? 16u : 0u;   // dynamic LDS bytes per blob float4
-
-// k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463)
-// RT_GEN_BLOCK: k_generate's workgroup (a divisor of BLOCK).  Claims stay per BLOCK-slot group (the
-// scan k_bookkeep makes over k_shade's blocks): a wave's claims start at its group's claim_base plus the
-// free slots of the group's earlier waves, whichever workgroup they are in.
-#ifndef RT_GEN_BLOCK
-#define RT_GEN_BLOCK BLOCK
-#endif
-constexpr int GEN_BLOCK = RT_GEN_BLOCK;
-static_assert(BLOCK % GEN_BLOCK == 0 && GEN_BLOCK % 64 == 0, "k_generate's workgroup divides BLOCK");
-__global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
+// k_generate — render_tile's per-sample ray setup (RT/raytracer.cpp:409-463).  It reads only the
+// sampler tables and the ray prologue's tables, which stay in HBM and are read through L2 and the
+// scalar cache: a block needs no LDS copy of the scene, so it skips that copy, its barrier and its
+// LDS footprint.
+__global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                         Counters* cnt, int cur) {
     // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
     // splat them.  Their NEE contributions from k_connect are in by now.
-#if RT_GEN_PRIO
-    __builtin_amdgcn_s_setprio(RT_GEN_PRIO);        // measurement switch: generate waves' issue priority
-#endif
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const uint32_t lane = __lane_id(), wave = (slot >> 6) & (uint32_t)(BLOCK / 64 - 1);   // wave in the group
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
     // Each wave's survivors fill its first slots; the rest take new paths, claiming consecutive
     // sample numbers in slot order from the scan of the free counts k_bookkeep made (no atomics):
     // the block's first claim, the free slots of the block's earlier waves, the lane's rank.
-    // The claim and the claimed sample's pixel are loaded first (RT_GEN_HOIST), so their round trips
+    // The claim and the claimed sample's pixel are loaded first, so their round trips
     // overlap the splat's below instead of waiting behind its stores.
     const uint32_t first = 64u - pool.free_w[wbase];
     uint32_t before = 0;
@@ -1658,7 +1531,6 @@ __global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settin
     const bool active = !none_left && want && (unsigned long long)claim < remaining;
     const unsigned long long k = cnt->next_sample + claim;
     uint32_t x = 0, y = 0, s = 0, p = 0;
-#if RT_GEN_HOIST
     if (active) {
         if (fp.list_xy) {
             x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
@@ -1675,7 +1547,6 @@ __global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settin
             x = xy & 0xFFFFu; y = xy >> 16; s = pass;
         }
     }
-#endif
     // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
     // splat them.  Their NEE contributions from k_connect are in by now.
     if (lane < pool.fin_w[wbase]) {
@@ -1690,32 +1561,12 @@ __global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settin
         if (want) pool.state[slot] = S_FREE;
         return;
     }
-#if RT_GEN_LDS_SCENE
-    const DevScene sc = scene_in_lds(sc_g, lds_scene);
-#else
-    const DevScene& sc = sc_g;       // nothing generate reads lives in the LDS copy (see RT_GEN_LDS_SCENE)
-#endif
+    const DevScene& sc = sc_g;       // nothing generate reads lives in the LDS copy of the scene
     if (want && !active) pool.state[slot] = S_FREE;
     bool enqueue = false, cast = false;
     V3 nro = {0, 0, 0}, nrd = {0, 0, 0};
     Prologue pro = {};
     if (active) {
-#if !RT_GEN_HOIST
-        if (fp.list_xy) {
-            x = fp.list_xy[2*k]; y = fp.list_xy[2*k + 1]; s = fp.list_s[k];
-        } else {
-            uint32_t pass;
-            if (k < 0x100000000ull && fp.px_m) {             // a multiply-high when k fits 32 bits
-                pass = div_pixels((uint32_t)k, fp.px_m);
-                p = (uint32_t)k - pass*fp.pixels;
-            } else {
-                pass = (uint32_t)(k / fp.pixels);
-                p = (uint32_t)(k % fp.pixels);
-            }
-            const uint32_t xy = fp.pix_xy[p];                // the tile list's pixel p (k_pixel_map)
-            x = xy & 0xFFFFu; y = xy >> 16; s = pass;
-        }
-#endif
         uint32_t canonical = fp.frame_count + s;
         uint32_t tile = tile_of(fp, x, y);
         Rng rng = random_seed(sample_seed(fp.total_frame_index, fp.frame_count, tile, y*fp.w + x, canonical));
@@ -1745,14 +1596,14 @@ __global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settin
         pool.ray_o[slot] = make_float4(jcp.x, jcp.y, jcp.z, __uint_as_float(x | (y << 16)));
         pool.ray_d[slot] = make_float4(rd.x, rd.y, rd.z, __uint_as_float(fp.list_xy ? (uint32_t)k : s));
         cast = st.max_bounce_count > 0;
-        if (!RT_GEN_LEAN || !cast) {
+        if (!cast) {
             pool.thr[slot] = make_float4(1.0f, 1.0f, 1.0f, vig);
             pool.L[slot] = make_float4(0.0f, 0.0f, 0.0f, !cast ? vig : __uint_as_float(pack_flags(0, 1, 0)));
         }
         pool.prev_n[slot] = make_float2(0.0f, __uint_as_float(p));
         pool.rng[slot] = make_uint4(rng.e0, rng.e1, rng.e2, rng.e3);
         // material_stack[0] = &air: level 0 is never stored; k_shade reads it as sc.air_id
-        pool.state[slot] = cast ? (RT_GEN_LEAN ? S_NEW : S_TRACE) : S_DONE;   // max_bounce_count == 0: nothing to trace
+        pool.state[slot] = cast ? S_NEW : S_DONE;   // max_bounce_count == 0: nothing to trace
         if (cast) {
             pro = ray_prologue(sc, jcp, rd, FLT_MAX_, false, 0u);
             pool.hit[slot] = make_float4(pro.t, __uint_as_float(pro.code), 0.0f, 0.0f);
@@ -1761,11 +1612,22 @@ __global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settin
     }
     // new paths that enter the BVH go to the current extension queue behind the survivors
     const uint32_t shard = blockIdx.x % NSHARD;
-    __shared__ uint32_t tally[(GEN_BLOCK / 64 + 2)*1];
+    __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
+    __shared__ uint32_t wcalls[BLOCK / 64];         // the camera rays' mesh instances reached (rt_stats::traversal)
+    {
+        const uint32_t wsum = __ockl_wfred_add_u32(pro.calls);
+        if (lane == 0) wcalls[wave] = wsum;
+    }
     const bool tp[1] = {enqueue};
     uint32_t* const tc[1] = {&cnt->ext_count[cur][shard][0]};
     uint32_t tpos[1], ttot[1];
-    block_tally<GEN_BLOCK, 1>(tp, tc, tpos, ttot, tally);
+    block_tally<BLOCK, 1>(tp, tc, tpos, ttot, tally);
+    if (threadIdx.x == 0) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; ++w) c += wcalls[w];
+        if (c) atomicAdd(&cnt->trav[shard][TV_CALLS], (unsigned long long)c);
+    }
     const uint32_t pos = tpos[0];
     if (enqueue) {
         float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + pos);
@@ -1782,47 +1644,24 @@ __global__ void __launch_bounds__(GEN_BLOCK) k_generate(DevScene sc_g, rt_settin
 // Persistent waves: each wave grabs CHUNK queue items with one atomic and
 // refills lanes whose query has finished from that chunk (Aila & Laine 2009,
 // for 64-wide waves), so lanes do not idle behind the wave's longest ray.
-#ifndef RT_TB
-#define RT_TB 256
-#endif
-constexpr int TB = RT_TB;
-#ifndef RT_CHUNK
-#define RT_CHUNK 256
-#endif
-constexpr uint32_t CHUNK = RT_CHUNK;
-#ifndef RT_STEPS_PER_REFILL
-#define RT_STEPS_PER_REFILL 8
-#endif
-#ifndef RT_STEPS_PER_REFILL_SHADOW
-#define RT_STEPS_PER_REFILL_SHADOW RT_STEPS_PER_REFILL
-#endif
-constexpr int STEPS_PER_REFILL = RT_STEPS_PER_REFILL;
-constexpr int STEPS_PER_REFILL_SHADOW = RT_STEPS_PER_REFILL_SHADOW;
+constexpr int TB = 256;                     // threads per persistent trace block
+constexpr uint32_t CHUNK = 256;             // queue items a wave takes per fetch
+constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 
 // 4 waves per SIMD (128 VGPRs): the BVH4 step wants ~138, i.e. 3 waves; the few
 // spilled values cost less than the lost occupancy (C3: 5446 vs 5389 Mrays/s)
-#ifndef RT_TRACE_WAVES
-#define RT_TRACE_WAVES 4
-#endif
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_TRACE_WAVES)))
-#ifndef RT_TRACE_PRIO
-#define RT_TRACE_PRIO 1
-#endif
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
-// DIAG (rt_scene_config::debug_traversal): count each query's steps for the longest-traversal report
-// (a separate instantiation: the counter is one more VGPR for the whole kernel)
-template <bool OCC, bool LST, bool DIAG>
-__global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill, int diag,
+template <bool OCC, bool LST>
+__global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill,
                                                               int fuse) {
     if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
-#if RT_TRACE_PRIO
     // trace waves are latency bound and issue little; shade waves sharing the SIMD are
     // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
     // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
-    __builtin_amdgcn_s_setprio(RT_TRACE_PRIO);
-#endif
+    __builtin_amdgcn_s_setprio(1);
     __shared__ uint2 lds_stack[STACK_LDS*TB];
     Stack st;
     st.lds = lds_stack; st.spill = spill; st.lane = threadIdx.x; st.block = TB;
@@ -1838,23 +1677,13 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     uint32_t chunk_next = 0, chunk_end = 0;
     bool exhausted = false, active = false;
     uint32_t item = 0;
-    uint32_t steps = 0;
     Traversal<OCC, LST> tr;
+    StepCounts<LST> tally;
+    static_assert(STEPS_PER_REFILL < 16, "StepCounts' 4-bit fields");
     auto finish = [&]() {
-        if (DIAG) {                                   // RT_DEBUG_TRAVERSAL: longest traversals
-            atomicMax(&cnt->max_steps[OCC ? 1 : 0], steps);
-            if (steps > 20000u) {
-                float* w = cnt->worst_ray[OCC ? 1 : 0];
-                w[0] = tr.wo.x; w[1] = tr.wo.y; w[2] = tr.wo.z;
-                w[3] = tr.wd.x; w[4] = tr.wd.y; w[5] = tr.wd.z; w[6] = 0.0f; w[7] = (float)steps;
-            }
-        }
-#ifdef RT_STEP_STATS
-        ++tr.stat[7];
-#endif
         if (OCC) {
             if (!tr.occluded) {
-                const uint32_t slot = RT_SH_STAGE ? pool.sh_dst[item] : pool.sh_slot[item];
+                const uint32_t slot = pool.sh_dst[item];
                 const float4 c = ldnt(&pool.sh_c[item]);
                 float4* const dst = (slot & SH_FIN) ? &pool.fin_L[slot & ~SH_FIN] : &pool.nx.L[slot];
                 float4 L = ldnt(dst);
@@ -1897,78 +1726,44 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
             if (!active && rank < avail) {
                 item = chunk_next + rank;
-                if (OCC && RT_SH_STAGE) item = pool.sh_slot[item];   // the k_shade slot that staged the ray
+                if (OCC) item = pool.sh_slot[item];               // the k_shade slot that staged the ray
                 const float4* q = (OCC ? pool.sh_rec : pool.ext_rec[cur]) + REC_Q*(size_t)item;
                 const float4 o = ldnt(&q[0]), d = ldnt(&q[1]), iv = ldnt(&q[2]);
                 if (!OCC) item = __float_as_uint(o.w);            // the path's slot
                 tr.init_rec(sc, st, ld3(o), ld3(d), ld3(iv), d.w, OCC ? __float_as_uint(o.w) : 0u, __float_as_uint(iv.w));
-                if (DIAG) steps = 0;
                 if (tr.mode == TM_DONE) finish(); else active = true;
             }
             chunk_next += min((uint32_t)__popcll(idle), avail);
             idle = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;
-#ifdef RT_STEP_STATS
-        if (lane == (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) tr.stat[1] += 64*(OCC ? STEPS_PER_REFILL_SHADOW : STEPS_PER_REFILL);
-#endif
         if (active) {
-            for (int k = 0; k < (OCC ? STEPS_PER_REFILL_SHADOW : STEPS_PER_REFILL); ++k) {
-                if (DIAG) ++steps;
+            for (int k = 0; k < STEPS_PER_REFILL; ++k) {
                 if (!tr.step(sc, st)) { finish(); active = false; break; }
             }
         }
+        tally.acc = tr.acc; tr.acc = 0;
+        tally.flush();                                  // every lane is here
     }
-#ifdef RT_STEP_STATS
-    for (int i = 0; i < 8; ++i) atomicAdd(&cnt->step_stats[OCC ? 1 : 0][i], (unsigned long long)tr.stat[i]);
-#endif
+    tally.commit(cnt->trav[blockIdx.x % NSHARD], OCC ? 1 : 0);
 }
 
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
-#if defined(RT_SHADE_MAX_WAVES)
-#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(1, RT_SHADE_MAX_WAVES)))
-#elif defined(RT_SHADE_WAVES)
-#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu(RT_SHADE_WAVES)))
-#elif RT_SHADE_STASH
 // 8 waves per SIMD (64 VGPRs) for the default instantiation (scene in LDS, no environment NEE),
 // which fits them without spills; the others need 66-67 and keep 7
 #define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((IN_LDS && !ENV) ? 8 : 7)))
-#else
-#define RT_SHADE_ATTR
-#endif
-#if RT_SHADE_PROF
-// Measurement build only (-DRT_SHADE_PROF=1): wave time per k_shade section, s_memtime
-// cycles summed over waves (the max over a wave's lanes: a divergent section costs the
-// wave whether one lane or all take it); printed to stderr after every frame.
-enum { SP_LOAD, SP_GEOM, SP_EMIS, SP_FRES, SP_REFL, SP_REFR, SP_NEE, SP_IND, SP_RR, SP_SKY, SP_SHPRO, SP_CPRO,
-       SP_STORE, SP_TAIL, SP_TOTAL, SP_N };
-__device__ unsigned long long g_shade_prof[SP_N + 1];
-#define SP_MARK(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#define SP_ADD(i, a) prof[i] += __builtin_amdgcn_s_memtime() - (a)
-#else
-#define SP_MARK(v)
-#define SP_ADD(i, a)
-#endif
 // One bounce of advanced_integrator (RT/integrators.cpp:612-815) for a path whose closest hit
 // is h: emission / MIS, Beer absorption, Fresnel, reflect / refract / diffuse with NEE (the
 // shadow ray is returned, not traced) and Russian roulette.  Shared by k_shade (one bounce per
 // launch) and k_drain (a path's remaining bounces in one launch), so both compute the same bits.
 // The material stack lives at pool.mstack[level*n + slot].  Returns true when the path ends.
-#if RT_SHADE_PROF
-#define SP_PARAM , unsigned long long* prof
-#define SP_PASS , prof
-#else
-#define SP_PARAM
-#define SP_PASS
-#endif
 template <bool ENV>
 RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerState& ss, const Pool& pool,
                        uint32_t slot, const Hit& h, V3& ro, V3& rd, V3& thr, V3& total, float& prev_pdf,
                        uint32_t& bounce, uint32_t& is_spec, int32_t& at, Rng& rng, bool& cast_shadow,
-                       V3& sh_o, V3& sh_d, V3& sh_c, float& sh_t, uint32_t& sh_light SP_PARAM) {
+                       V3& sh_o, V3& sh_d, V3& sh_c, float& sh_t, uint32_t& sh_light) {
     bool done = false;
     if (h.code != RT_HIT_MISS) {
-        SP_MARK(t_geom);
         V3 I, N;
         uint32_t surf_id;
         Ray ray; ray.o = ro; ray.d = rd;
@@ -1989,13 +1784,11 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
         }
         const rt_material mi = sc.materials[mi_id];
         const rt_material mt = sc.materials[mt_id];
-        SP_ADD(SP_GEOM, t_geom);
         if (mi.is_participating_medium) {                                  // Beer :640-649
             V3 ab = {d_expf(-mi.absorb.x*t), d_expf(-mi.absorb.y*t), d_expf(-mi.absorb.z*t)};
             thr = mul(thr, ab);
         }
         if (mt.flags & RT_MATERIAL_EMISSIVE) {                             // :651-670
-            SP_MARK(t_emis);
             bool allow = (!st.next_event_estimation ||
                           ((st.caustics || (bounce < 2)) && is_spec));
             if (allow) {
@@ -2008,9 +1801,7 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
                 total = add(total, mul(smul(rcp_cr(mis_pdf), thr), rv3(mt.emission_color)));
             }
             done = true;
-            SP_ADD(SP_EMIS, t_emis);
         } else {
-            SP_MARK(t_fres);
             float eta_i = mi.ior, eta_t = mt.ior;
             float eta = eta_i / eta_t;
             float cos_t;
@@ -2018,9 +1809,7 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
             float reflect_test = sample_1d(sc, ss, rng, S_Reflectance, bounce);
             refl = lerpf_(refl, 1.0f, mt.metallic);
             is_spec = 1;
-            SP_ADD(SP_FRES, t_fres);
             if (reflect_test < refl) {                                      // reflect :684-696
-                SP_MARK(t_refl);
                 V3 nd = reflect(rd, N);
                 if (mt.roughness > 0.0f) {
                     V3 rs = random_in_unit_sphere(rng);
@@ -2028,9 +1817,7 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
                 }
                 ro = add(I, smul(EPSILON, nd)); rd = nd;
                 thr = mul(thr, lerp3(v3s(1.0f), rv3(mt.albedo), mt.metallic));
-                SP_ADD(SP_REFL, t_refl);
             } else if (mt.is_participating_medium) {                       // refract :698-717
-                SP_MARK(t_refr);
                 if (inside) {
                     if (at > 0) --at;
                 } else if (at < 63) {
@@ -2039,9 +1826,7 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
                 }
                 V3 fd = add(smul(eta, rd), muls(N, (eta*cos_i - cos_t)));
                 ro = add(I, muls(fd, EPSILON)); rd = fd;
-                SP_ADD(SP_REFR, t_refr);
             } else {                                                        // diffuse :718-790
-                SP_MARK(t_nee);
                 is_spec = 0;
                 V3 albedo = evaluate_material(mt, I);
                 V3 brdf = smul(1.0f / PI_32, albedo);
@@ -2111,8 +1896,6 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
                         }
                     }
                 }
-                SP_ADD(SP_NEE, t_nee);
-                SP_MARK(t_ind);
                 V2 s2 = sample_2d(sc, ss, rng, S_IndirectLighting, bounce); // indirect :777-789
                 V3 R;
                 if (st.importance_sample_diffuse) {
@@ -2124,15 +1907,12 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
                 }
                 thr = mul(thr, brdf);
                 ro = add(I, muls(N, EPSILON)); rd = R;
-                SP_ADD(SP_IND, t_ind);
             }
             if (st.russian_roulette && !is_spec) {                          // RR :801-811
-                SP_MARK(t_rr);
                 float p = clampf_(max3(thr), 0.1f, 0.9f);
                 float e = sample_1d(sc, ss, rng, S_Roulette, bounce);
                 if (e > p) done = true;
                 else thr = muls(thr, rcp_cr(p));
-                SP_ADD(SP_RR, t_rr);
             }
         }
         if (!done) {
@@ -2141,7 +1921,6 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
             if (bounce >= st.max_bounce_count) done = true;
         }
     } else {
-        SP_MARK(t_sky);
         if (ENV) {
             // a path leaving a diffuse vertex (which sampled the environment in its NEE):
             // balance heuristic against that pdf; without MIS the NEE alone carries it
@@ -2163,7 +1942,6 @@ RT_D bool shade_bounce(const DevScene& sc, const rt_settings& st, const SamplerS
             total = add(total, mul(thr, sample_sky(sc, rd)));             // miss :812-815
         }
         done = true;
-        SP_ADD(SP_SKY, t_sky);
     }
     return done;
 }
@@ -2173,10 +1951,6 @@ template <bool IN_LDS, bool ENV>
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur, int sparse, int fuse) {
     if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
-#if RT_SHADE_PROF
-    unsigned long long prof[SP_N] = {};
-    SP_MARK(t_start);
-#endif
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     // The slot's state and path record are loaded before the scene copy, whatever the
     // state: the three round trips (state, record, LDS blob) overlap instead of running
@@ -2203,7 +1977,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         state0 = pool.state[slot];
         load_path();
     }
-    if (RT_GEN_LEAN && state0 == S_NEW) {                              // a camera ray (k_generate)
+    if (state0 == S_NEW) {                              // a camera ray (k_generate)
         new_path_records(fp, st, d4, t4, L4);
         state0 = S_TRACE;
     }
@@ -2220,25 +1994,15 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     // that end here
     const bool made_fin = slot < pool.n && state0 == S_DONE;
     const unsigned long long made_fin_mask = __ballot(made_fin);
-#if RT_SHADE_STASH
-    // pixel, sample key, vignette and tile-list pixel: written out only at the end, so they wait in
-    // LDS (the thread's own entry, no barrier) instead of registers across the bounce and prologues
+    // pixel, sample key, vignette and tile-list pixel (`meta`): written out only at the end, so they
+    // wait in LDS (the thread's own entry, no barrier) instead of registers across the bounce and
+    // the prologues
     __shared__ uint4 stash[BLOCK];
+    __shared__ uint8_t sh_calls[BLOCK];             // the shadow prologue's mesh instances reached
     if (valid || made_fin)
         stash[threadIdx.x] = make_uint4(__float_as_uint(o4.w), __float_as_uint(d4.w), __float_as_uint(t4.w),
                                         __float_as_uint(pn2.y));
-#define SH_META_PIXEL(m) __uint_as_float((m).x)
-#define SH_META_KEY(m) __uint_as_float((m).y)
-#define SH_META_VIG(m) __uint_as_float((m).z)
-#define SH_META_P(m) __uint_as_float((m).w)
-#else
-#define SH_META_PIXEL(m) o4.w
-#define SH_META_KEY(m) d4.w
-#define SH_META_VIG(m) t4.w
-#define SH_META_P(m) pn2.y
-#endif
     if (valid) {
-        SP_MARK(t_load);
         Rng rng = {r4.x, r4.y, r4.z, r4.w};
         V3 ro = ld3(o4), rd = ld3(d4);
         V3 thr = ld3(t4), total = ld3(L4);
@@ -2253,51 +2017,46 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         SamplerState ss = {px, py, canonical, st.sampling_strategy};
         Hit h;
         h.t = h4.x; h.code = __float_as_uint(h4.y); h.tri = __float_as_uint(h4.z); h.v = h4.w; h.w = hw;
-        SP_ADD(SP_LOAD, t_load);
         done = shade_bounce<ENV>(sc, st, ss, pool, slot, h, ro, rd, thr, total, prev_pdf, bounce, is_spec, at, rng,
-                                 cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light SP_PASS);
-#if RT_SHADE_EARLY
+                                 cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light);
         // The survivor's state that the two prologues below do not change goes out now, so the
         // throughput, RNG and flags are not held in registers across them (total_color and the
-        // hit record follow the prologues).
+        // hit record follow the prologues).  The wave's paths that continue go, in slot order, to
+        // the front of its 64 slots in the other buffer (pool.nx): a ballot, no barrier.  The next
+        // k_generate fills the rest.  A path that ends goes to the wave's finished array.
         cont = !done;
-#if RT_SHADE_STASH
-        const uint4 meta = stash[threadIdx.x];
-#else
-        const uint4 meta = {};
-#endif
+        const uint4 meta = stash[threadIdx.x];          // pixel, key, vignette, tile-list pixel
         {
             const unsigned long long smask = __ballot(cont);
             nslot = (slot & ~63u) + (uint32_t)__popcll(smask & ((1ull << __lane_id()) - 1ull));
         }
         if (cont) {
-            stnt(&pool.nx.ray_o[nslot], make_float4(ro.x, ro.y, ro.z, SH_META_PIXEL(meta)));
-            stnt(&pool.nx.ray_d[nslot], make_float4(rd.x, rd.y, rd.z, SH_META_KEY(meta)));
-            stnt(&pool.nx.thr[nslot], make_float4(thr.x, thr.y, thr.z, SH_META_VIG(meta)));
-            stnt(&pool.nx.prev_n[nslot], make_float2(prev_pdf, SH_META_P(meta)));
+            stnt(&pool.nx.ray_o[nslot], make_float4(ro.x, ro.y, ro.z, __uint_as_float(meta.x)));
+            stnt(&pool.nx.ray_d[nslot], make_float4(rd.x, rd.y, rd.z, __uint_as_float(meta.y)));
+            stnt(&pool.nx.thr[nslot], make_float4(thr.x, thr.y, thr.z, __uint_as_float(meta.z)));
+            stnt(&pool.nx.prev_n[nslot], make_float2(prev_pdf, __uint_as_float(meta.w)));
             stnt(&pool.nx.rng[nslot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
             pool.nx.state[nslot] = S_TRACE;
+            // the material stack moves with the path (levels 1..at; level 0 is the implicit air)
             for (int32_t lv = 1; lv <= at; ++lv)
                 pool.nx.mstack[(size_t)lv*pool.n + nslot] = pool.mstack[(size_t)lv*pool.n + slot];
         }
         const unsigned long long fm = made_fin_mask | __ballot(done);
         if (done) {                                        // everything but total_color
             const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
-            stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(SH_META_KEY(meta)), __float_as_uint(SH_META_P(meta))));
-            stnt(&pool.fin_px[fidx], __float_as_uint(SH_META_PIXEL(meta)));
+            stnt(&pool.fin_k[fidx], make_uint2(meta.y, meta.w));
+            stnt(&pool.fin_px[fidx], meta.x);
         }
-        const float vig = SH_META_VIG(meta);
+        const float vig = __uint_as_float(meta.z);
         const uint32_t nflags = pack_flags(bounce, is_spec, (uint32_t)at);
-#endif
         if (cast_shadow) {
             // intersect_shadow_ray (:756): planes and the top level here; only rays that meet
             // a mesh are queued for k_trace<true>.  Nothing else adds to total_color after the
             // NEE term in a bounce, so adding it here keeps the reference's order (:768).
-            SP_MARK(t_shpro);
             spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
+            sh_calls[threadIdx.x] = (uint8_t)spro.calls;   // counted at the tail, not held in a register
             shadow = !spro.occluded && spro.bvh;
             if (!spro.occluded && !spro.bvh) total = add(total, sh_c);
-#if RT_SH_STAGE
             if (shadow) {                                  // staged at the slot (Pool::sh_rec)
                 float4* q = pool.sh_rec + REC_Q*(size_t)slot;
                 stnt(&q[0], make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light)));
@@ -2305,65 +2064,19 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
                 stnt(&q[2], make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist)));
                 stnt(&pool.sh_c[slot], make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f));
             }
-#endif
-            SP_ADD(SP_SHPRO, t_shpro);
         }
-#if RT_SHADE_EARLY
-        SP_MARK(t_store);
         if (cont) stnt(&pool.nx.L[nslot], make_float4(total.x, total.y, total.z, __uint_as_float(nflags)));
         if (done) {
             const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
             stnt(&pool.fin_L[fidx], make_float4(total.x, total.y, total.z, vig));
         }
-        SP_ADD(SP_STORE, t_store);
         nro = ro; nrd = rd;
         if (cont) {                                        // next bounce's intersect_scene: planes + top level here
-            SP_MARK(t_cpro);
             cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
             enq = cpro.bvh;
             stnt(&pool.nx.hit[nslot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
-            SP_ADD(SP_CPRO, t_cpro);
         }
-#else
-        cont = !done;
-        nro = ro; nrd = rd;
-        if (cont) {                                        // next bounce's intersect_scene: planes + top level here
-            SP_MARK(t_cpro);
-            cpro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
-            enq = cpro.bvh;
-            SP_ADD(SP_CPRO, t_cpro);
-        }
-        // The wave's paths that continue go, in slot order, to the front of its 64 slots in the
-        // other buffer (pool.nx): a ballot, no barrier.  The next k_generate fills the rest.
-        const unsigned long long smask = __ballot(cont);
-        nslot = (slot & ~63u) + (uint32_t)__popcll(smask & ((1ull << __lane_id()) - 1ull));
-        SP_MARK(t_store);
-        // A path that ends here goes to the wave's finished array; its state is not written back.
-        const unsigned long long fm = made_fin_mask | __ballot(done);
-        if (done) {
-            const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
-            stnt(&pool.fin_L[fidx], make_float4(total.x, total.y, total.z, t4.w));
-            stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(d4.w), __float_as_uint(pn2.y)));
-            stnt(&pool.fin_px[fidx], __float_as_uint(o4.w));
-        }
-        if (cont) {
-            stnt(&pool.nx.hit[nslot], make_float4(cpro.t, __uint_as_float(cpro.code), 0.0f, 0.0f));
-            stnt(&pool.nx.ray_o[nslot], make_float4(ro.x, ro.y, ro.z, o4.w));
-            stnt(&pool.nx.ray_d[nslot], make_float4(rd.x, rd.y, rd.z, d4.w));
-            stnt(&pool.nx.thr[nslot], make_float4(thr.x, thr.y, thr.z, t4.w));
-            stnt(&pool.nx.L[nslot], make_float4(total.x, total.y, total.z,
-                                                __uint_as_float(pack_flags(bounce, is_spec, (uint32_t)at))));
-            stnt(&pool.nx.prev_n[nslot], make_float2(prev_pdf, pn2.y));
-            stnt(&pool.nx.rng[nslot], make_uint4(rng.e0, rng.e1, rng.e2, rng.e3));
-            pool.nx.state[nslot] = S_TRACE;
-            // the material stack moves with the path (levels 1..at; level 0 is the implicit air)
-            for (int32_t lv = 1; lv <= at; ++lv)
-                pool.nx.mstack[(size_t)lv*pool.n + nslot] = pool.mstack[(size_t)lv*pool.n + slot];
-        }
-        SP_ADD(SP_STORE, t_store);
-#endif
     }
-    SP_MARK(t_tail);
     const int nxt = cur ^ 1;
     const uint32_t shard = blockIdx.x % NSHARD;
     // The wave's paths that end here (or were made finished: max_bounce_count 0) go to the front of
@@ -2373,14 +2086,10 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const unsigned long long fmask = __ballot(fin);
     const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fmask & ((1ull << __lane_id()) - 1ull));
     if (made_fin) {                                 // L = 0 with the vignette in .w (k_generate)
-#if RT_SHADE_STASH
         const uint4 fmeta = stash[threadIdx.x];
-#else
-        const uint4 fmeta = {};
-#endif
         stnt(&pool.fin_L[fidx], pool.L[slot]);
-        stnt(&pool.fin_k[fidx], make_uint2(__float_as_uint(SH_META_KEY(fmeta)), __float_as_uint(SH_META_P(fmeta))));
-        stnt(&pool.fin_px[fidx], __float_as_uint(SH_META_PIXEL(fmeta)));
+        stnt(&pool.fin_k[fidx], make_uint2(fmeta.y, fmeta.w));
+        stnt(&pool.fin_px[fidx], fmeta.x);
     }
     const unsigned long long cmask = __ballot(cont);
     if (__lane_id() == 0) {
@@ -2388,11 +2097,26 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         pool.fin_w[slot >> 6] = (uint32_t)__popcll(fmask);
     }
     __shared__ uint32_t tally[(BLOCK / 64 + 2)*6];
+    // the wave's mesh instances reached by its prologues (rt_stats::traversal), next bounce | shadow << 16
+    // (at most 64 x 63 each); published before the tally's first barrier, added up after it
+    __shared__ uint32_t wcalls[BLOCK / 64];
+    {
+        const uint32_t c = cpro.calls | ((cast_shadow ? (uint32_t)sh_calls[threadIdx.x] : 0u) << 16);
+        const uint32_t wsum = __ockl_wfred_add_u32(c);
+        if (__lane_id() == 0) wcalls[threadIdx.x >> 6] = wsum;
+    }
     const bool tp[6] = {enq, shadow, cont, cast_shadow, fin, slot < pool.n && !cont};
     uint32_t* const tc[6] = {&cnt->ext_count[nxt][shard][0], &cnt->shadow_count[shard][0], &cnt->alive[shard][0],
                              &cnt->cast[1][shard][0], &cnt->unsplat[shard][0], nullptr};
     uint32_t tpos[6], ttot[6];
     block_tally<BLOCK, 6>(tp, tc, tpos, ttot, tally);
+    if (threadIdx.x == 0) {
+        uint32_t c0 = 0, c1 = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; ++w) { c0 += wcalls[w] & 0xFFFFu; c1 += wcalls[w] >> 16; }
+        if (c0) atomicAdd(&cnt->trav[shard][TV_CALLS], (unsigned long long)c0);
+        if (c1) atomicAdd(&cnt->trav[shard][TV_N + TV_CALLS], (unsigned long long)c1);
+    }
     const uint32_t pos = tpos[0];
     if (enq) {
         float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + pos);
@@ -2403,30 +2127,10 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const uint32_t spos = shard*pool.shard_cap + tpos[1];
     if (shadow) {
         // the NEE term goes to the survivor's L in pool.nx, or to the finished entry
-#if RT_SH_STAGE
         pool.sh_slot[spos] = slot;
         pool.sh_dst[slot] = cont ? nslot : (SH_FIN | fidx);
-#else
-        pool.sh_slot[spos] = cont ? nslot : (SH_FIN | fidx);
-        float4* q = pool.sh_rec + REC_Q*(size_t)spos;
-        stnt(&q[0], make_float4(sh_o.x, sh_o.y, sh_o.z, __uint_as_float(sh_light)));
-        stnt(&q[1], make_float4(sh_d.x, sh_d.y, sh_d.z, sh_t));
-        stnt(&q[2], make_float4(spro.inv_d.x, spro.inv_d.y, spro.inv_d.z, __uint_as_float(spro.mlist)));
-        stnt(&pool.sh_c[spos], make_float4(sh_c.x, sh_c.y, sh_c.z, 0.0f));
-#endif
     }
     if (threadIdx.x == 0) pool.free_n[blockIdx.x] = ttot[5];
-#if RT_SHADE_PROF
-    SP_ADD(SP_TAIL, t_tail);
-    SP_ADD(SP_TOTAL, t_start);
-    if (blockIdx.x % 128 == 0)      // a sample of the waves: the atomics must not load the memory system
-    for (int i = 0; i < SP_N; ++i) {
-        unsigned long long v = prof[i];
-        for (int m = 32; m; m >>= 1) { const unsigned long long u = __shfl_xor(v, m); v = u > v ? u : v; }
-        if ((threadIdx.x & 63) == 0) atomicAdd(&g_shade_prof[i], v);
-    }
-    if (blockIdx.x % 128 == 0 && (threadIdx.x & 63) == 0) atomicAdd(&g_shade_prof[SP_N], 1ull);
-#endif
 }
 
 
@@ -2467,17 +2171,11 @@ __global__ void __launch_bounds__(BLOCK) k_drain_list(Pool pool, Counters* cnt) 
 // ~220-VGPR wave finds room on one SIMD much sooner than a 256-thread block does on four at once beside
 // the other partitions' kernels (those empty launches cost up to ~1 ms each in the iterations before
 // the drain).
-#ifndef RT_DRAIN_TB
-#define RT_DRAIN_TB 64
-#endif
-constexpr int DTB = RT_DRAIN_TB;
+constexpr int DTB = 64;
 template <bool LST, bool ENV>
 __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
                                                uint2* spill) {
     if (!cnt->fused || cnt->done) return;                              // uniform
-#if RT_DRAIN_PRIO
-    __builtin_amdgcn_s_setprio(RT_DRAIN_PRIO);      // measurement switch: drain waves' issue priority
-#endif
     __shared__ uint2 lds_stack[STACK_LDS*DTB];
     Stack stk;
     stk.lds = lds_stack; stk.spill = spill; stk.lane = threadIdx.x; stk.block = DTB;
@@ -2490,7 +2188,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     uint32_t chunk_next = 0, chunk_end = 0;
     bool exhausted = false, active = false, fresh = false;
-    uint32_t n_closest = 0, n_shadow = 0, n_traced = 0, n_traced_sh = 0;
+    uint32_t n_closest = 0, n_shadow = 0, n_traced = 0, n_traced_sh = 0, n_calls[2] = {0, 0};
     // the lane's path
     uint32_t slot = 0;
     V3 ro = {0, 0, 0}, rd = {0, 0, 0}, thr = {0, 0, 0}, total = {0, 0, 0};
@@ -2499,6 +2197,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
     int32_t at = 0;
     Rng rng = {0, 0, 0, 0};
     Prologue pro = {};
+    StepCounts<LST> tally[2];                       // closest, shadow
     for (;;) {
         // idle lanes take the next live slots
         unsigned long long idle = __ballot(!active);
@@ -2533,7 +2232,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                 float4 t4 = ldnt(&pool.thr[slot]), L4 = ldnt(&pool.L[slot]);
                 const float2 pn2 = ldnt(&pool.prev_n[slot]);
                 const uint4 r4 = ldnt(&pool.rng[slot]);
-                if (RT_GEN_LEAN && pool.state[slot] == S_NEW) new_path_records(fp, st, d4, t4, L4);
+                if (pool.state[slot] == S_NEW) new_path_records(fp, st, d4, t4, L4);
                 ro = ld3(o4); rd = ld3(d4); thr = ld3(t4); total = ld3(L4); vig = t4.w;
                 prev_pdf = pn2.x; p = __float_as_uint(pn2.y);
                 const uint32_t flags = __float_as_uint(L4.w);
@@ -2550,8 +2249,10 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
         // the closest hit: the ray prologue (the same result k_shade / k_generate stored with the
         // path), then the BVH walk for a ray that meets a mesh
         if (active) pro = ray_prologue(sc, ro, rd, FLT_MAX_, false, 0u);
-        // a fresh path's ray is counted already (k_bookkeep: alive / cast, and its queue entry)
+        // a fresh path's ray is counted already (k_bookkeep: alive / cast, and its queue entry; its
+        // prologue's mesh instances by the k_shade / k_generate that made it)
         n_traced += (active && !fresh && pro.bvh) ? 1u : 0u;
+        n_calls[0] += (active && !fresh) ? pro.calls : 0u;
         fresh = false;
         Hit h;
         h.t = pro.t; h.code = pro.code; h.tri = 0; h.v = 0.0f; h.w = 0.0f;
@@ -2562,9 +2263,12 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                 tr.init_rec(sc, stk, ro, rd, pro.inv_d, pro.t, 0u, pro.mlist);
                 tracing = tr.mode != TM_DONE;
             }
-            while (__ballot(tracing)) {
+            for (int k = 1; __ballot(tracing); ++k) {
                 if (tracing && !tr.step(sc, stk)) tracing = false;
+                if (k % STEPS_PER_REFILL == 0) { tally[0].acc = tr.acc; tr.acc = 0; tally[0].flush(); }
             }
+            tally[0].acc = tr.acc;
+            tally[0].flush();
             if (active && pro.bvh && tr.code != RT_HIT_MISS) h = tr.result();
         }
         // one bounce
@@ -2575,17 +2279,15 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
         if (active) {
             const uint32_t canonical = fp.frame_count + (fp.list_xy ? fp.list_s[key] : key);
             const SamplerState ss = {pixel & 0xFFFFu, pixel >> 16, canonical, st.sampling_strategy};
-#if RT_SHADE_PROF
-            unsigned long long prof[SP_N] = {};
-#endif
             done = shade_bounce<ENV>(sc, st, ss, pool, slot, h, ro, rd, thr, total, prev_pdf, bounce, is_spec, at, rng,
-                                     cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light SP_PASS);
+                                     cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light);
         }
         // intersect_shadow_ray (:756): the prologue, then the BVH walk; the NEE term is added last
         // in the bounce, as k_connect adds it (:768)
         {
             Prologue spro = {};
             if (cast_shadow) spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
+            n_calls[1] += cast_shadow ? spro.calls : 0u;
             Traversal<true, LST> tr;
             bool tracing = cast_shadow && !spro.occluded && spro.bvh;
             n_traced_sh += tracing ? 1u : 0u;
@@ -2593,9 +2295,12 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                 tr.init_rec(sc, stk, sh_o, sh_d, spro.inv_d, sh_t, sh_light, spro.mlist);
                 tracing = tr.mode != TM_DONE;
             }
-            while (__ballot(tracing)) {
+            for (int k = 1; __ballot(tracing); ++k) {
                 if (tracing && !tr.step(sc, stk)) tracing = false;
+                if (k % STEPS_PER_REFILL == 0) { tally[1].acc = tr.acc; tr.acc = 0; tally[1].flush(); }
             }
+            tally[1].acc = tr.acc;
+            tally[1].flush();
             if (cast_shadow && !spro.occluded && (!spro.bvh || !tr.occluded)) total = add(total, sh_c);
         }
         n_shadow += cast_shadow ? 1u : 0u;
@@ -2620,6 +2325,14 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
         if (c[2]) atomicAdd(&cnt->traced_rays[0], c[2]);
         if (c[3]) atomicAdd(&cnt->traced_rays[1], c[3]);
     }
+    unsigned long long* trav = cnt->trav[blockIdx.x % NSHARD];
+    tally[0].commit(trav, 0);
+    tally[1].commit(trav, 1);
+    const uint32_t calls0 = __ockl_wfred_add_u32(n_calls[0]), calls1 = __ockl_wfred_add_u32(n_calls[1]);
+    if (lane == 0) {
+        if (calls0) atomicAdd(&trav[TV_CALLS], (unsigned long long)calls0);
+        if (calls1) atomicAdd(&trav[TV_N + TV_CALLS], (unsigned long long)calls1);
+    }
 }
 
 // k_resolve — splat_filter as a gather (RT/raytracer.cpp:187-259, :476-488).
@@ -2641,38 +2354,27 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
 // strips read fewer records per pixel ((8 + 4)/8 against (4 + 4)/4 source rows) but make half
 // as many threads: the full C3 frame resolves in 21.7 ms instead of 24.0 (frame +1.2 %, A/B
 // twice), one rank's eighth in 9.8 ms instead of 5.5 (too few waves to cover the latency).
-#ifndef RT_RES_RY
-#define RT_RES_RY 4
-#endif
-#ifndef RT_RES_RY_TALL
-#define RT_RES_RY_TALL 8
-#endif
-#ifndef RT_RES_TALL_PIXELS
-#define RT_RES_TALL_PIXELS 1600000u
-#endif
-constexpr uint32_t RES_TALL_PIXELS = RT_RES_TALL_PIXELS;
-#ifndef RT_RES_U
-#define RT_RES_U 8
-#endif
-constexpr int RES_U = RT_RES_U;        // sample records loaded ahead per thread
+constexpr int RES_RY = 4, RES_RY_TALL = 8;
+constexpr uint32_t RES_TALL_PIXELS = 1600000u;   // rt_scene_config::resolve_tall_pixels' default
+constexpr int RES_U = 8;               // sample records loaded ahead per thread
 constexpr int RES_BX = 64, RES_BY = 4;
-template <int RES_RY>
+template <int RY>
 __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
     __shared__ float lut[512];
     for (int i = threadIdx.x; i < 512; i += RES_BX*RES_BY) lut[i] = fp.cache_size ? fp.lut[i] : 0.0f;
     __syncthreads();
     const int X = blockIdx.x*RES_BX + (threadIdx.x % RES_BX);
-    const int Y0 = (blockIdx.y*RES_BY + (threadIdx.x / RES_BX))*RES_RY;
+    const int Y0 = (blockIdx.y*RES_BY + (threadIdx.x / RES_BX))*RY;
     const int W = (int)fp.w, H = (int)fp.h;
     if (X >= W || Y0 >= H) return;
     const int ks = fp.cache_size ? fp.kernel_size : 0;
     const float kscale = ks ? (float)(fp.cache_size - 1) / (float)ks : 0.0f;
     const int TW = (int)fp.tile_w, TH = (int)fp.tile_h;
     const int x0 = max(X - ks, 0), x1 = min(X + ks, W - 1);
-    const int y0 = max(Y0 - ks, 0), y1 = min(Y0 + RES_RY - 1 + ks, H - 1);
-    float4 acc[RES_RY];
+    const int y0 = max(Y0 - ks, 0), y1 = min(Y0 + RY - 1 + ks, H - 1);
+    float4 acc[RY];
 #pragma unroll
-    for (int r = 0; r < RES_RY; ++r) acc[r] = (Y0 + r < H) ? fp.accum[(size_t)(Y0 + r)*W + X] : make_float4(0, 0, 0, 0);
+    for (int r = 0; r < RY; ++r) acc[r] = (Y0 + r < H) ? fp.accum[(size_t)(Y0 + r)*W + X] : make_float4(0, 0, 0, 0);
     const size_t P = fp.pixels;
     const float dx = (float)(X);
     for (int ty = y1 / TH; ty >= y0 / TH; --ty) {
@@ -2686,7 +2388,7 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
             const int xa = max(x0, min_x), xb = min(x1, min_x + TW - 1);
             for (int y = ya; y <= yb; ++y) {
                 // strip pixels whose window holds row y: Y0 + r in [y - ks, y + ks]
-                const int rlo = max(y - ks - Y0, 0), rhi = min(y + ks - Y0, RES_RY - 1);
+                const int rlo = max(y - ks - Y0, 0), rhi = min(y + ks - Y0, RY - 1);
                 for (int x = xa; x <= xb; ++x) {
                     const size_t p = (size_t)base + (size_t)(y - min_y)*twid + (size_t)(x - min_x);
                     if (ks) {
@@ -2694,7 +2396,7 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
                         auto splat = [&](const float4 c, const float jy) {
                             const float fx = lut[(int)fabsf(0.5f + kscale*(fdx - c.w))];
 #pragma unroll
-                            for (int r = 0; r < RES_RY; ++r) {
+                            for (int r = 0; r < RY; ++r) {
                                 if (r < rlo || r > rhi) continue;
                                 const float dy = (float)(Y0 + r - y);
                                 const float fy = lut[(int)fabsf(0.5f + kscale*(dy - jy))];
@@ -2726,11 +2428,11 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
                         }
                     } else {                                   // box filter: the pixel's own samples, (result, 1)
                         const int r = y - Y0;
-                        if (r < 0 || r >= RES_RY || x != X) continue;
+                        if (r < 0 || r >= RY || x != X) continue;
                         for (uint32_t s = 0; s < fp.spp; ++s) {
                             const float4 c = fp.samp_rgbx[(size_t)s*P + p];
 #pragma unroll
-                            for (int q = 0; q < RES_RY; ++q)
+                            for (int q = 0; q < RY; ++q)
                                 if (q == r) {
                                     acc[q].x = acc[q].x + c.x; acc[q].y = acc[q].y + c.y;
                                     acc[q].z = acc[q].z + c.z; acc[q].w = acc[q].w + 1.0f;
@@ -2742,7 +2444,7 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
         }
     }
 #pragma unroll
-    for (int r = 0; r < RES_RY; ++r)
+    for (int r = 0; r < RY; ++r)
         if (Y0 + r < H) fp.accum[(size_t)(Y0 + r)*W + X] = acc[r];
 }
 
@@ -2754,7 +2456,6 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
 // [res_from, res_to) the workgroup stages the records of the block's source region (the
 // block plus the filter radius on every side, from the owned tiles only) into LDS with
 // one coalesced load each, and every thread sums its strip's (2r+1)^2 windows out of LDS.
-// The next pass's records are loaded into registers while the current one is summed.
 //
 // Per output pixel the sum runs pass by pass, and inside a pass over the window rows and
 // columns in ascending order, from the value the buffer held: deterministic, and the same
@@ -2767,24 +2468,17 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
 //
 // Partition k resolves its own pass range into its own buffer (the caller's for k = 0),
 // so partitions never write the same buffer; k_combine_partials adds them up at the end.
-// RT_RES_PREFETCH 1: the next pass's records load into registers while this pass is summed (r02-r03;
-// 120 VGPRs); 0 (default, r03b) loads each pass at its start: 90 VGPRs, and the blocks find room
-// beside the other partitions' kernels sooner (C3 +0.2 %, C4 +0.6 %), the load latency exposed per pass
-#ifndef RT_RES_PREFETCH
-#define RT_RES_PREFETCH 0
-#endif
+// Each pass's records are loaded at the start of that pass (r03b): 90 VGPRs, and the blocks find
+// room beside the other partitions' kernels sooner than with the next pass loading into registers
+// while this one is summed (120 VGPRs; C3 +0.2 %, C4 +0.6 %), at the cost of the load latency
+// exposed once per pass.
 constexpr int TR_W = 64, TR_H = 16, TR_THREADS = 256, TR_ROWS = TR_H / (TR_THREADS / TR_W);
 __host__ __device__ constexpr int tr_stage_slots(int ks) { return ((TR_W + 2*ks)*(TR_H + 2*ks) + TR_THREADS - 1) / TR_THREADS; }
 __host__ __device__ constexpr size_t tr_lds_bytes(int ks) {
     return (size_t)(TR_W + 2*ks)*(TR_H + 2*ks)*(16 + 4) + 512*4;
 }
-#ifdef RT_RES_WAVES
-#define RT_RES_ATTR __attribute__((amdgpu_waves_per_eu(RT_RES_WAVES)))
-#else
-#define RT_RES_ATTR
-#endif
 template <int KSMAX>
-__global__ void __launch_bounds__(TR_THREADS) RT_RES_ATTR k_resolve_tiles(FrameParams fp, Pool pool, const Counters* cnt,
+__global__ void __launch_bounds__(TR_THREADS) k_resolve_tiles(FrameParams fp, Pool pool, const Counters* cnt,
                                                                const uint32_t* blocks, float4* dst) {
     const uint32_t s0 = cnt->res_from, s1 = cnt->res_to;
     if (s0 >= s1) return;
@@ -2847,13 +2541,8 @@ __global__ void __launch_bounds__(TR_THREADS) RT_RES_ATTR k_resolve_tiles(FrameP
     const float kscale = ks ? (float)(fp.cache_size - 1) / (float)ks : 0.0f;
     const int xa = max(X - ks, 0), xb = min(X + ks, W - 1);
     const int ya = max(Y0 - ks, 0), yb = min(Y0 + TR_ROWS - 1 + ks, H - 1);
-#if RT_RES_PREFETCH
-    load_pass(s0);
-#endif
     for (uint32_t s = s0; s < s1; ++s) {
-#if !RT_RES_PREFETCH
         load_pass(s);
-#endif
         __syncthreads();                                    // the previous pass's sums are done with LDS
 #pragma unroll
         for (int k = 0; k < NST; ++k) {
@@ -2861,9 +2550,6 @@ __global__ void __launch_bounds__(TR_THREADS) RT_RES_ATTR k_resolve_tiles(FrameP
             if (i < N) { srgb[i] = pc[k]; sjy[i] = pj[k]; }
         }
         __syncthreads();
-#if RT_RES_PREFETCH
-        if (s + 1 < s1) load_pass(s + 1);                   // in flight while this pass is summed
-#endif
         if (!col_in) continue;
         for (int sy = ya; sy <= yb; ++sy) {
             const int rlo = max(sy - ks - Y0, 0), rhi = min(sy + ks - Y0, TR_ROWS - 1);
@@ -2935,21 +2621,13 @@ enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
 // cast0: max_bounce_count > 0, so every sample claimed this iteration casts a camera ray (k_bookkeep counts
 // them from the claims; k_generate keeps no counter for them)
 struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0; };
-// Two workgroup sizes, picked per frame by the partition's pool (RT_BK_LARGE_POOL): a pool of 4M paths or
+// Two workgroup sizes, picked per frame by the partition's pool (BK_LARGE_POOL): a pool of 4M paths or
 // more (a whole 1080p frame: 8.4M) takes the 256-thread build (156 VGPRs: 4 waves that find room beside
 // the other partitions' kernels sooner), a smaller one (a rank's share of a multi-GPU frame: 3.3M) the
 // 1024-thread build (62 VGPRs, 16 waves on one CU).  A/B (profiles/r03b_ab.txt section 14): 256 threads
 // give the full C3 frame +0.5 to +0.9 % and C4 +1.2 to +1.5 %, but rank 0 of 8 -1.9 to -2.8 %.
-#ifndef RT_BK_THREADS
-#define RT_BK_THREADS 1024
-#endif
-#ifndef RT_BK_THREADS_LARGE
-#define RT_BK_THREADS_LARGE 256
-#endif
-#ifndef RT_BK_LARGE_POOL
-#define RT_BK_LARGE_POOL (4u << 20)
-#endif
-constexpr int BK_THREADS_SMALL = RT_BK_THREADS, BK_THREADS_LARGE = RT_BK_THREADS_LARGE;
+constexpr int BK_THREADS_SMALL = 1024, BK_THREADS_LARGE = 256;
+constexpr uint32_t BK_LARGE_POOL = 4u << 20;
 template <int BK_THREADS>
 __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
                                                          ResPlan plan) {
@@ -2967,11 +2645,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
     // The free counts' loads go out first, so they overlap the counter work below.
     // Up to BK_EMAX entries per thread (pools up to 32k blocks, 8.4M paths) are loaded at once into
     // registers, all in flight, and the claims are written from them; a loop covers larger pools.
-#ifndef RT_BK_REG
-#define RT_BK_REG 1
-#endif
-    // RT_BK_REG 0: no register copy (two passes over the counts, the second from L2)
-    constexpr uint32_t BK_EMAX = RT_BK_REG ? 32*(1024 / BK_THREADS) : 1;
+    constexpr uint32_t BK_EMAX = 32*(1024 / BK_THREADS);
     const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
     const uint32_t lo = t*E, hi = min(lo + E, nblocks);
     uint32_t v[BK_EMAX];
@@ -3484,9 +3158,9 @@ int ensure_pool(Partition& pt, uint32_t n) {
     e |= alloc((void**)&p.ext_rec[1], 16*REC_Q*Q);
     e |= alloc((void**)&p.state, N);
     e |= alloc((void**)&p.sh_slot, 4*Q);
-    e |= alloc((void**)&p.sh_rec, 16*REC_Q*(RT_SH_STAGE ? N : Q));
-    e |= alloc((void**)&p.sh_c, 16*(RT_SH_STAGE ? N : Q));
-    if (RT_SH_STAGE) e |= alloc((void**)&p.sh_dst, 4*N);
+    e |= alloc((void**)&p.sh_rec, 16*REC_Q*N);
+    e |= alloc((void**)&p.sh_c, 16*N);
+    e |= alloc((void**)&p.sh_dst, 4*N);
     if (e) { free_pool(pt); return RT_ERROR_OUT_OF_MEMORY; }
     p.n = n;
     return RT_OK;
@@ -3531,16 +3205,13 @@ inline bool debug_timing() { static const bool on = getenv("RT_DEBUG_TIMING") !=
 // full frame gains from 8M paths (6.3M 239.3 / 239.4, 8.4M 236.7 / 237.6, 10.5M 237.7 / 238.8, 12.6M
 // 239.8 / 240.3 ms): the upper bound is 4 x 2^21 (rank 0 of 2 at 8.4M: 128.7 -> 128.8 / 129.2, unchanged).
 struct FrameShape { int nparts; uint32_t pool_n; };
-#ifndef RT_POOL_DIV
-#define RT_POOL_DIV 5ull
-#endif
 FrameShape frame_shape(const rt_scene* s, unsigned long long total, uint32_t passes) {
     FrameShape f;
     f.nparts = s->cfg.partitions > 0 ? std::min(MAX_PARTITIONS, (int)s->cfg.partitions) : 4;
     if (passes) f.nparts = std::max(1, std::min<int>(f.nparts, (int)passes));   // partitions own whole passes
     uint32_t pool_n = s->cfg.path_pool > 0 ? (uint32_t)s->cfg.path_pool : g_pool_override;
     if (!pool_n) {
-        const unsigned long long want = total / (unsigned long long)f.nparts / RT_POOL_DIV;
+        const unsigned long long want = total / (unsigned long long)f.nparts / 5ull;
         pool_n = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>(want, 1ull << 21), 4ull << 21);
     }
     // small frames: one partition, pool no larger than the work
@@ -3591,8 +3262,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     const FrameShape shape = frame_shape(s, total, listed ? 0u : sp.passes);
     const int nparts = shape.nparts;
     const uint32_t pool_n = shape.pool_n;
-    // k_bookkeep's workgroup size by the pool (RT_BK_LARGE_POOL, see k_bookkeep)
-    const bool bk_large = pool_n >= RT_BK_LARGE_POOL;
+    // k_bookkeep's workgroup size by the pool (BK_LARGE_POOL, see k_bookkeep)
+    const bool bk_large = pool_n >= BK_LARGE_POOL;
     auto launch_bookkeep = [bk_large](Counters* c, const Pool& pl, uint32_t nblocks, int cur, int phase, ResPlan plan,
                                       hipStream_t q) {
         if (bk_large) k_bookkeep<BK_THREADS_LARGE><<<1, BK_THREADS_LARGE, 0, q>>>(c, pl, nblocks, cur, phase, plan);
@@ -3714,7 +3385,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         // iteration after k_bookkeep set Counters::fused, whose extend / shade / connect then exit
         const int fuse = (r.near && fuse_paths) ? 1 : 0;
         b(RT_KERNEL_GENERATE);
-        k_generate<<<r.grid*(BLOCK / GEN_BLOCK), GEN_BLOCK, GEN_LDS_Q_SCALE*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
+        k_generate<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE);
         if (fuse) {
             k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
@@ -3727,11 +3398,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             }
         }
         b(RT_KERNEL_EXTEND);
-        if (diag) {
-            if (s->ds.listed_only) k_trace<false, true, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-            else k_trace<false, false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-        } else if (s->ds.listed_only) k_trace<false, true, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-        else k_trace<false, false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         if (env) {
             if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
@@ -3742,11 +3410,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (diag) {
-            if (s->ds.listed_only) k_trace<true, true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-            else k_trace<true, false, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-        } else if (s->ds.listed_only) k_trace<true, true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
-        else k_trace<true, false, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, diag, fuse);
+        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         e(RT_KERNEL_CONNECT);
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
@@ -3854,6 +3519,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         }
     }
     Counters sum = {};
+    unsigned long long tv[2*TV_N] = {};
     uint64_t iters = 0;
     for (int k = 0; k < nparts; ++k) {
         const Counters& c = s->part[k].cnt_host[run[k].final_buf];
@@ -3861,30 +3527,31 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         sum.shadow_rays += c.shadow_rays;
         sum.traced_rays[0] += c.traced_rays[0];
         sum.traced_rays[1] += c.traced_rays[1];
-        for (int a = 0; a < 2; ++a) {
-            for (int i = 0; i < 8; ++i) sum.step_stats[a][i] += c.step_stats[a][i];
-            if (c.max_steps[a] >= sum.max_steps[a]) {
-                sum.max_steps[a] = c.max_steps[a];
-                memcpy(sum.worst_ray[a], c.worst_ray[a], sizeof(sum.worst_ray[a]));
-            }
-        }
+        for (int sh = 0; sh < NSHARD; ++sh)
+            for (int i = 0; i < 2*TV_N; ++i) tv[i] += c.trav[sh][i];
         iters = std::max(iters, run[k].iters);
     }
-    if (diag) {
-        const Counters& c = sum;
-        for (int k = 0; k < 2; ++k) {
-            const unsigned long long* v = c.step_stats[k];
-            if (!v[1]) continue;
-            fprintf(stderr, "[rt] %s step stats: rays %llu lane-steps %llu wave-steps*64 %llu (SIMD eff %.3f) steps/ray %.2f "
-                    "pops/ray %.2f interior/ray %.2f leaf/ray %.2f records/ray %.2f\n",
-                    k ? "shadow" : "closest", v[7], v[0], v[1], (double)v[0]/v[1], (double)v[0]/v[7],
-                    (double)v[2]/v[7], (double)v[4]/v[7], (double)v[5]/v[7], (double)v[6]/v[7]);
-        }
-        for (int k = 0; k < 2; ++k)
-            fprintf(stderr, "[rt] %s: max steps %u; worst ray o=(%.9g %.9g %.9g) d=(%.9g %.9g %.9g) max_t=%.9g steps=%.0f\n",
-                    k ? "shadow" : "closest", c.max_steps[k], c.worst_ray[k][0], c.worst_ray[k][1], c.worst_ray[k][2],
-                    c.worst_ray[k][3], c.worst_ray[k][4], c.worst_ray[k][5], c.worst_ray[k][6], c.worst_ray[k][7]);
+    // TraversalStats per kind (rt_stats::traversal, rt_abi.h)
+    rt_traversal_stats ts[2] = {};
+    uint64_t steps[2] = {};
+    for (int a = 0; a < 2; ++a) {
+        const unsigned long long* v = tv + a*TV_N;
+        // the prologue's walk reaches the instances (ray_prologue); a scene whose top level is too large
+        // for the prologue has it walked by the trace kernels, whose entries are then the calls
+        ts[a].mesh_intersection_count = s->ds.top_seq ? v[TV_CALLS] : v[TV_ENTRIES];
+        ts[a].mesh_bvh_traversals = v[TV_ENTRIES] + v[TV_NODES] + v[TV_TRIS];
+        ts[a].mesh_node_traversals = v[TV_NODES];
+        ts[a].mesh_leaf_traversals = v[TV_LEAVES];
+        steps[a] = ts[a].mesh_bvh_traversals + v[TV_TOP];
     }
+    if (diag)                                       // rt_scene_config::debug_traversal
+        for (int a = 0; a < 2; ++a)
+            fprintf(stderr, "[rt] %s queries: %llu mesh instances reached, %llu entered, %llu mesh steps (%llu BVH4 "
+                    "nodes, %llu leaves entered), %llu trace steps\n", a ? "shadow" : "closest",
+                    (unsigned long long)ts[a].mesh_intersection_count, tv[a*TV_N + TV_ENTRIES],
+                    (unsigned long long)ts[a].mesh_bvh_traversals,
+                    (unsigned long long)ts[a].mesh_node_traversals, (unsigned long long)ts[a].mesh_leaf_traversals,
+                    (unsigned long long)steps[a]);
     if (stats) {
         memset(stats, 0, sizeof(*stats));
         stats->closest_hit_rays = sum.closest_rays;
@@ -3895,6 +3562,10 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         for (int k = 0; k < RT_KERNEL_COUNT; ++k) { stats->kernel_ms[k] = kms[k]; stats->kernel_launches[k] = klaunch[k]; }
         stats->traced_rays[0] = sum.traced_rays[0];
         stats->traced_rays[1] = sum.traced_rays[1];
+        for (int a = 0; a < 2; ++a) {
+            stats->traversal[a] = ts[a];
+            stats->trace_steps[a] = steps[a];
+        }
     }
     return RT_OK;
 }
@@ -4012,15 +3683,39 @@ int check_config(const rt_scene_config* c) {
 }
 
 // The test-override environment variables, applied once at rt_scene_upload (never per frame).
-void config_from_env(rt_scene_config& c) {
-    if (const char* e = getenv("RT_SPLAT")) c.splat_mode = atoi(e);
-    if (const char* e = getenv("RT_PARTITIONS")) c.partitions = std::max(1, std::min(MAX_PARTITIONS, atoi(e)));
-    if (const char* e = getenv("RT_FUSE_PATHS")) c.fuse_paths = (int64_t)strtoull(e, nullptr, 10);
-    if (const char* e = getenv("RT_SPLAT_CHUNK")) c.splat_chunk = std::max(1, atoi(e));
-    if (const char* e = getenv("RT_SPLAT_RING")) c.splat_ring = std::max(1, atoi(e));
-    if (const char* e = getenv("RT_SAMPLE_BUDGET_GB")) c.sample_budget_gb = std::max(0.0, atof(e));
-    if (const char* e = getenv("RT_RES_TALL_PIXELS")) c.resolve_tall_pixels = (int64_t)strtoull(e, nullptr, 0);
-    if (getenv("RT_DEBUG_TRAVERSAL")) c.debug_traversal = 1;
+// A value that is not a whole number (RT_SPLAT=exact) is an error, not a silent 0: false, with
+// the variable named in the error text.
+bool config_from_env(rt_scene_config& c) {
+    bool ok = true;
+    auto num = [&](const char* name, long long lo, long long hi, long long& out) {
+        const char* e = getenv(name);
+        if (!e) return false;
+        char* end = nullptr;
+        errno = 0;
+        const long long v = strtoll(e, &end, 0);
+        if (!*e || *end || errno || v < lo || v > hi) {
+            set_error(std::string("rt_scene_upload: bad ") + name + "=" + e);
+            ok = false;
+            return false;
+        }
+        out = v;
+        return true;
+    };
+    long long v = 0;
+    if (num("RT_SPLAT", RT_SPLAT_STREAM, RT_SPLAT_ATOMIC, v)) c.splat_mode = (int32_t)v;
+    if (num("RT_PARTITIONS", 1, MAX_PARTITIONS, v)) c.partitions = (int32_t)v;
+    if (num("RT_FUSE_PATHS", 0, 0xFFFFFFFFll, v)) c.fuse_paths = v;
+    if (num("RT_SPLAT_CHUNK", 1, 1 << 20, v)) c.splat_chunk = (int32_t)v;
+    if (num("RT_SPLAT_RING", 1, 1 << 20, v)) c.splat_ring = (int32_t)v;
+    if (const char* e = getenv("RT_SAMPLE_BUDGET_GB")) {
+        char* end = nullptr;
+        const double g = strtod(e, &end);
+        if (!*e || *end || !(g >= 0.0)) { set_error(std::string("rt_scene_upload: bad RT_SAMPLE_BUDGET_GB=") + e); ok = false; }
+        else c.sample_budget_gb = g;
+    }
+    if (num("RT_RES_TALL_PIXELS", 0, 1ll << 40, v)) c.resolve_tall_pixels = v;
+    if (num("RT_DEBUG_TRAVERSAL", 0, 1, v)) c.debug_traversal = (int32_t)v;
+    return ok;
 }
 
 }  // namespace
@@ -4088,7 +3783,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     rt_scene* s = new rt_scene();
     s->device = device;
     s->cfg = default_config();
-    config_from_env(s->cfg);
+    if (!config_from_env(s->cfg)) { delete s; return RT_ERROR_INVALID; }
     if ((err = check_config(&s->cfg))) { delete s; return err; }
     DevScene& ds = s->ds;
     auto fail = [&](int e) { rt_scene_free(s); return e; };
@@ -4140,10 +3835,9 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         if ((err = upload(s, tl.data(), tl.size(), &ds.bvh))) return fail(err);
     }
     if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
-    std::vector<float4> top_seq_host, leaf_rec_host;
     {
         const char* env = getenv("RT_TOP_PROLOGUE");              // 0: the trace kernels walk the top level
-        std::vector<float4>& seq = top_seq_host;
+        std::vector<float4> seq;
         uint32_t len = 0;
         if (!(env && env[0] == '0')) seq = top_sequences(d->bvh_nodes, d->bvh_node_count, d->bvh_index_count, len);
         ds.top_seq = nullptr; ds.top_seq_len = 0; ds.mlist_max = MLIST_MAX;
@@ -4178,7 +3872,6 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 set_error("mesh BVH node out of range"); return fail(RT_ERROR_INVALID);
             }
         }
-#if RT_MESH_BVH4
         if (M.node_count) {
             const rt_bvh_node& r0 = M.nodes[0];
             if (r0.count) {
@@ -4192,9 +3885,6 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 mesh_depth = std::max(mesh_depth, need + 1);
             }
         }
-#else
-        mesh_depth = std::max(mesh_depth, tree_depth(M.nodes, M.node_count));
-#endif
         for (uint32_t t = 0; t < M.triangle_count; ++t) {
             const rt_v3* v = M.triangles + 3*(size_t)t;
             tris.push_back(make_float4(v[0].x, v[0].y, v[0].z, 0.0f));
@@ -4242,11 +3932,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 const rt_mesh& M = d->meshes[p.mesh_index];
                 rt_bvh_node rn = {};
                 if (M.node_count) rn = M.nodes[0];
-#if RT_MESH_BVH4
                 const uint32_t root = root4[p.mesh_index];
-#else
-                const uint32_t root = pack_node(0u, rn.left_first, rn.count, rn.split_axis);
-#endif
                 q[3] = make_float4(u2f(pi), u2f(p.type), u2f(meshes[p.mesh_index].node_offset), u2f(meshes[p.mesh_index].tri_offset));
                 q[4] = make_float4(u2f(root), rn.bv_p.x, rn.bv_p.y, rn.bv_p.z);
                 q[5] = make_float4(rn.bv_r.x, rn.bv_r.y, rn.bv_r.z, 0.0f);
@@ -4260,7 +3946,6 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         }
         rec.resize(rec.size() + FETCH_Q, make_float4(0, 0, 0, 0));
         if ((err = upload(s, rec.data(), rec.size(), &ds.leaf_rec))) return fail(err);
-        leaf_rec_host = rec;
     }
     if ((err = upload(s, meshes.data(), meshes.size(), &ds.meshes))) return fail(err);
     tris.resize(tris.size() + FETCH_Q, make_float4(0, 0, 0, 0));
@@ -4323,21 +4008,9 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         put(BLOB_INV, inv.data(), inv.size()*sizeof(M34));
         put(BLOB_FWD, fwd.data(), fwd.size()*sizeof(M34));
         put(BLOB_LIGHTS, d->lights, (size_t)d->light_count*sizeof(uint32_t));
-#if RT_PROLOGUE_SCALAR
         // the prologue reads the top-level sequences and leaf records from HBM through the scalar
-        // cache (scene_in_lds does not rebase them): not copied into LDS (C3: 5 KB -> ~2 KB per block)
-        put(BLOB_TOP_SEQ, nullptr, 0);
-        put(BLOB_LEAF_REC, nullptr, 0);
-#else
-        put(BLOB_TOP_SEQ, top_seq_host.data(), top_seq_host.size()*sizeof(float4));
-        put(BLOB_LEAF_REC, leaf_rec_host.data(), (size_t)d->bvh_index_count*LEAF_REC_Q*sizeof(float4));
-#endif
+        // cache, and the strata table stays in HBM (both read through L2): not copied into LDS
         put(BLOB_MESHES, meshes.data(), meshes.size()*sizeof(DevMesh));
-#if RT_LDS_STRATA
-        put(BLOB_STRATA, rt_dev_strata_tab, sizeof(rt_dev_strata_tab));
-#else
-        put(BLOB_STRATA, nullptr, 0);
-#endif
         const char* env = getenv("RT_LDS_SCENE");               // 0: the kernels read the tables from HBM
         ds.blob = nullptr; ds.blob_q = 0;
         if (blob.size() <= 16*(size_t)LDS_SCENE_Q && !(env && env[0] == '0')) {
@@ -4351,7 +4024,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("hipGetDeviceProperties"); return fail(RT_ERROR_DEVICE); }
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
         s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
         // Persistent trace blocks: 75 % of one full-occupancy wave of blocks (RT_TRACE_GRID_PCT).
         // Four partitions run their trace launches side by side; a full grid per launch left
@@ -4715,25 +4388,13 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
     if (prof_resolve) { HIP_OK(hipEventCreate(&e0)); HIP_OK(hipEventCreate(&e1)); HIP_OK(hipEventRecord(e0, stream)); }
     const uint64_t tall_px = s->cfg.resolve_tall_pixels > 0 ? (uint64_t)s->cfg.resolve_tall_pixels : RES_TALL_PIXELS;
     const bool tall = fp.pixels >= tall_px;
-    const int rry = tall ? RT_RES_RY_TALL : RT_RES_RY;
+    const int rry = tall ? RES_RY_TALL : RES_RY;
     dim3 rgrid((w + RES_BX - 1) / RES_BX, (h + RES_BY*rry - 1) / (RES_BY*rry));
-    if (tall) k_resolve<RT_RES_RY_TALL><<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
-    else k_resolve<RT_RES_RY><<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
+    if (tall) k_resolve<RES_RY_TALL><<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
+    else k_resolve<RES_RY><<<rgrid, RES_BX*RES_BY, 0, stream>>>(fp);
     HIP_OK(hipGetLastError());
     if (prof_resolve) HIP_OK(hipEventRecord(e1, stream));
     HIP_OK(hipStreamSynchronize(stream));
-#if RT_SHADE_PROF
-    {
-        static const char* names[SP_N] = {"load", "geom", "emis", "fres", "refl", "refr", "nee", "ind", "rr", "sky",
-                                          "shpro", "cpro", "store", "tail", "total"};
-        unsigned long long v[SP_N + 1] = {}, zero[SP_N + 1] = {};
-        HIP_OK(hipMemcpyFromSymbol(v, HIP_SYMBOL(g_shade_prof), sizeof(v)));
-        HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_shade_prof), zero, sizeof(zero)));
-        fprintf(stderr, "shade_prof waves=%llu", v[SP_N]);
-        for (int i = 0; i < SP_N; ++i) fprintf(stderr, " %s=%.1f", names[i], (double)v[i] / (double)(v[SP_N] ? v[SP_N] : 1));
-        fprintf(stderr, " (cycles per wave)\n");
-    }
-#endif
     if (stats) {
         stats->splat_mode = sp.mode;
         stats->seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

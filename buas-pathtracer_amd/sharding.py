@@ -21,12 +21,13 @@ def owned_tiles(w, h, tile_w, tile_h, rank, world):
     return [t for t in range(tcx * tcy - 1, -1, -1) if t % world == rank]
 
 
-def render_frame_sharded(render_shard, accum, rank, world, group=None, scratch=None):
+def render_frame_sharded(render_shard, accum, rank, world, group=None, scratch=None, reduce=None):
     """render_shard(shard_index, shard_count, buf) ADDS this rank's tiles of one frame into
-    `buf` (a torch tensor shaped like `accum`).  With world > 1 the frame is rendered into
-    `scratch` (zeroed here; allocated if None), sum-reduced into rank 0 and added to rank 0's
-    `accum`; the other ranks' `accum` is left untouched.  Returns the render_shard result."""
-    if world == 1:
+    `buf` (a torch tensor shaped like `accum`).  With world > 1 (or `reduce` set: the same path at
+    one rank) the frame is rendered into `scratch` (zeroed here; allocated if None), sum-reduced
+    into rank 0 and added to rank 0's `accum`; the other ranks' `accum` is left untouched.
+    Returns the render_shard result."""
+    if not (world > 1 if reduce is None else reduce):
         return render_shard(rank, world, accum)
     import torch.distributed as dist
     buf = scratch if scratch is not None else accum.new_zeros(accum.shape)

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* ---------------------------------------------------------------- status */
 enum rt_status {
@@ -205,6 +205,36 @@ enum rt_kernel_id {                 /* wavefront stages, for rt_stats::kernel_ms
     RT_KERNEL_COUNT    = 6,
 };
 
+/* The reference's TraversalStats (RT/intersection.h:33-40): render_all_tiles hands them to its
+ * caller and zeroes them every frame (RT/raytracer.cpp:727-731); intersect_mesh counts them
+ * (RT/intersection.cpp:254, :378-380).  Here they are counted on the device, per frame, in this
+ * library's own walk, whose order and layout differ from the reference's in two documented ways
+ * (DESIGN.md section 3):
+ *   - the top level is walked in one fixed order with the planes, spheres and boxes tested before
+ *     any mesh BVH (the hits are the reference's), so t at a top-level node does not yet include
+ *     the mesh hits the reference's front-to-back walk would have found;
+ *   - mesh BVHs are BVH4s (each BVH2 interior node merged with its interior children), and a child
+ *     is box-tested when its parent is expanded instead of when it is popped.
+ * A shadow query that a mesh occludes is counted like any other (the reference returns before its
+ * traversal counts are added, RT/intersection.cpp:297-299). */
+typedef struct rt_traversal_stats {
+    /* intersect_mesh calls (RT/intersection.cpp:488, counted at :254): mesh instances a query's
+       top-level walk reaches -- the top-level leaf holding the instance passes its pop-time test
+       (:454), the instance is not the query's ignored light (:466), and no plane, sphere or box has
+       occluded a shadow query before it */
+    uint64_t mesh_intersection_count;
+    /* mesh BVH steps: each one round of 8 x 16-byte loads per lane -- an instance's entry (its
+       object-space ray, RT/intersection.cpp:472, and its root box test), a BVH4 interior node, or up
+       to two triangles of a leaf.  (Reference: BVH2 nodes taken from the stack, :274.) */
+    uint64_t mesh_bvh_traversals;
+    /* BVH4 interior nodes expanded: taken from the stack with their far-clip test passed.
+       (Reference: BVH2 interior nodes that pass their pop-time test, :358.) */
+    uint64_t mesh_node_traversals;
+    /* mesh BVH leaves entered: taken from the stack with their far-clip test passed -- the
+       reference's definition (:279); the BVH4 has the BVH2's leaves */
+    uint64_t mesh_leaf_traversals;
+} rt_traversal_stats;
+
 typedef struct rt_stats {
     uint64_t closest_hit_rays;      /* intersect_scene calls (RT/integrators.cpp:615)      */
     uint64_t shadow_rays;           /* intersect_shadow_ray calls (RT/integrators.cpp:756) */
@@ -220,6 +250,12 @@ typedef struct rt_stats {
     uint64_t traced_rays[2];
     int32_t  splat_mode;            /* rt_splat_mode the frame used (rt_render / rt_render_device) */
     int32_t  reserved;
+    /* TraversalStats of the frame (above) per query kind: [0] closest-hit (intersect_scene),
+       [1] shadow (intersect_shadow_ray); the reference's totals are the sums of the two */
+    rt_traversal_stats traversal[2];
+    /* trace steps per kind (every step of the extend / connect kernels and the fused drain,
+       top-level steps included): the fetch rounds of 128 B per lane the traversal roofline counts */
+    uint64_t trace_steps[2];
 } rt_stats;
 
 typedef struct rt_ray_query {       /* debug/parity entry: one ray for rt_debug_intersect */

@@ -514,27 +514,44 @@ static inline int ray_intersect_triangle(const Ray* ray, V3 a, V3 b, V3 c,
     return 1;
 }
 
-/* intersect_mesh, BVHStorage_Scalar path (RT/intersection.cpp:243-401). */
+/* TraversalStats (RT/intersection.h:33-40) as the reference counts them: TS_CALLS per intersect_mesh
+   call (RT/intersection.cpp:254); per traversal the nodes taken from the stack (:274), the interior
+   ones (:358) and the leaves (:279) that pass their pop-time test, added when the traversal ends
+   (:378-380) -- not when an occlusion query returns from inside it (:297-299). */
+enum { TS_CALLS, TS_BVH, TS_NODES, TS_LEAVES, TS_N };
+
+/* intersect_mesh, BVHStorage_Scalar path (RT/intersection.cpp:243-401).  ts: the reference's
+   TraversalStats of the query kind (or NULL); leaves_all: leaves entered, counted whether or not
+   the traversal returns early (the GPU walk's count, gpu_walk_query below; or NULL). */
 static int intersect_mesh(const rt_mesh* mesh, const Ray* ray, int occlusion, float* out_t,
-                          uint32_t* out_tri, V3* out_uvw, V3* out_a, V3* out_b, V3* out_c) {
+                          uint32_t* out_tri, V3* out_uvw, V3* out_a, V3* out_b, V3* out_c,
+                          uint64_t* ts, uint64_t* leaves_all) {
     uint32_t hit_tri = 0xFFFFFFFFu;
     uint32_t stack[64];
     uint32_t at = 0;
+    uint64_t trav = 0, nodes = 0, leaves = 0;
+    if (ts) ts[TS_CALLS]++;
     stack[at++] = 0;
     while (at > 0) {
         const rt_bvh_node* node = &mesh->nodes[stack[--at]];
+        ++trav;
         if (ray_intersect_bv(ray, node->bv_p, node->bv_r, *out_t)) {
             if (node->count) {
+                ++leaves;
                 uint32_t first = node->left_first;
                 for (uint32_t i = 0; i < node->count; ++i) {
                     const rt_v3* tri = &mesh->triangles[3*(size_t)(first + i)];
                     if (ray_intersect_triangle(ray, tri[0], tri[1], tri[2], out_t, out_uvw)) {
-                        if (occlusion) return 1;
+                        if (occlusion) {
+                            if (leaves_all) *leaves_all += leaves;
+                            return 1;
+                        }
                         *out_a = tri[0]; *out_b = tri[1]; *out_c = tri[2];
                         hit_tri = mesh->indices[first + i];
                     }
                 }
             } else {
+                ++nodes;
                 uint32_t left = node->left_first;
                 if (at + 2 > 64) return 0;    /* the reference overflows its stack[64] here (UB) */
                 if (ray->neg[node->split_axis]) { stack[at++] = left; stack[at++] = left + 1; }
@@ -542,6 +559,8 @@ static int intersect_mesh(const rt_mesh* mesh, const Ray* ray, int occlusion, fl
             }
         }
     }
+    if (ts) { ts[TS_BVH] += trav; ts[TS_NODES] += nodes; ts[TS_LEAVES] += leaves; }
+    if (leaves_all) *leaves_all += leaves;
     if (hit_tri != 0xFFFFFFFFu) { *out_tri = hit_tri; return 1; }
     return 0;
 }
@@ -559,9 +578,10 @@ typedef struct {
     V3 hit_p, n;
 } Hit;
 
-/* intersect_scene_internal (RT/intersection.cpp:411-598).  Returns 1 on hit. */
+/* intersect_scene_internal (RT/intersection.cpp:411-598).  Returns 1 on hit.  ts: TraversalStats
+   of the query kind (TS_*), or NULL. */
 static int intersect_scene_internal(const rt_scene_desc* scene, const Ray* ray, int occlusion,
-                                    uint32_t ignored, Hit* out) {
+                                    uint32_t ignored, Hit* out, uint64_t* ts) {
     float t = ray->max_t;
     int hit_kind = 0;
     uint32_t hit_index = 0;
@@ -594,7 +614,7 @@ static int intersect_scene_internal(const rt_scene_desc* scene, const Ray* ray, 
                             case RT_PRIMITIVE_BOX: hit_any = ray_intersect_box(&ir, v3(prim->p[0], prim->p[1], prim->p[2]), &t); break;
                             case RT_PRIMITIVE_MESH:
                                 hit_any = intersect_mesh(&scene->meshes[prim->mesh_index], &ir, occlusion, &t,
-                                                         &hit_tri, &uvw, &a, &b, &c);
+                                                         &hit_tri, &uvw, &a, &b, &c, ts, NULL);
                                 break;
                             default: break;
                         }
@@ -654,6 +674,137 @@ static int intersect_scene_internal(const rt_scene_desc* scene, const Ray* ray, 
     return hit_kind != 0;
 }
 
+/* ---------------------------------------------------------------------- */
+/* The MI355X library's walk, restated for its TraversalStats (rt_stats::traversal on the GPU;
+   DESIGN.md section 3).  Not the reference: the GPU tests the planes and the top level's spheres and
+   boxes before any mesh BVH (ray_prologue in buas-pathtracer_amd/csrc/rt_kernels.hip), so the mesh
+   instances it reaches and enters and the leaves it visits are counted in that order:
+     - the prologue walks the top level in one fixed order (octant 0: the left child first) with t
+       from the planes and the analytic primitives only; a mesh instance whose leaf passes is reached
+       (GW_CALLS: the GPU's mesh_intersection_count), and listed when its root box passes at that t;
+       an analytic occluder ends a shadow query there;
+     - a query with 1..mlist_max listed instances enters them in list order (GW_ENTRIES), each with
+       its BVH walked from the current t (GW_LEAVES: leaves taken from the stack with their far-clip
+       test passed), a shadow query ending at the first occluding instance;
+     - a query with more (MLIST_FULL), or every query of a scene whose top level is too large for the
+       prologue, walks the whole top level from the root in the reference's front-to-back order,
+       starting at the prologue's t, entering every mesh instance whose leaf passes (for the scene
+       whose top level is too large, these entries are the GPU's mesh_intersection_count).
+   The leaves are the BVH4's (the BVH2's leaves); the GPU's pruning of nodes that a ray with an
+   exactly-zero direction component cannot hit (bv_static) is not restated, so leaf counts may differ
+   by such rays' leaves. */
+enum { GW_CALLS, GW_ENTRIES, GW_LEAVES, GW_N };
+static int g_gw_on = 0;
+static uint32_t g_gw_mlist = 4;
+static int g_gw_top = 1;
+static uint64_t g_gw_acc[2][GW_N];
+static pthread_mutex_t g_gw_mu = PTHREAD_MUTEX_INITIALIZER;
+
+void oracle_gpu_walk_stats(int on, uint32_t mlist_max, int top_prologue) {
+    pthread_mutex_lock(&g_gw_mu);
+    g_gw_on = on != 0;
+    g_gw_mlist = mlist_max;
+    g_gw_top = top_prologue != 0;
+    memset(g_gw_acc, 0, sizeof(g_gw_acc));
+    pthread_mutex_unlock(&g_gw_mu);
+}
+
+void oracle_gpu_walk_result(uint64_t out[6]) {
+    pthread_mutex_lock(&g_gw_mu);
+    for (int k = 0; k < 2; ++k)
+        for (int i = 0; i < GW_N; ++i) out[k*GW_N + i] = g_gw_acc[k][i];
+    pthread_mutex_unlock(&g_gw_mu);
+}
+
+static void gw_add(const uint64_t g[2][GW_N]) {
+    if (!g_gw_on) return;
+    pthread_mutex_lock(&g_gw_mu);
+    for (int k = 0; k < 2; ++k)
+        for (int i = 0; i < GW_N; ++i) g_gw_acc[k][i] += g[k][i];
+    pthread_mutex_unlock(&g_gw_mu);
+}
+
+/* a mesh instance entered by the trace kernel: its object-space ray, its BVH from t */
+static int gw_mesh(const rt_scene_desc* sc, const rt_primitive* prim, const Ray* ray, int occ, float* t,
+                   uint64_t* g) {
+    Ray ir = transform_ray(ray, &sc->transforms[prim->transform_index].inverse);
+    uint32_t tri;
+    V3 uvw, a, b, c;
+    g[GW_ENTRIES]++;
+    return intersect_mesh(&sc->meshes[prim->mesh_index], &ir, occ, t, &tri, &uvw, &a, &b, &c, NULL, &g[GW_LEAVES]);
+}
+
+/* the top level walked with `neg` as the direction signs (the reference's order for the ray's own, the
+   prologue's for 0); list != NULL: the prologue (spheres and boxes tested, mesh instances reached, and
+   listed when their root box passes); NULL: the trace kernel (mesh instances entered, and counted as
+   reached when `calls`).  Returns 1 when a shadow query is occluded. */
+static int gw_top(const rt_scene_desc* sc, const Ray* ray, const int neg[3], int occ, uint32_t ignored, float* t,
+                  uint32_t* list, uint32_t* n, uint64_t* g, int calls) {
+    uint32_t stack[64];
+    uint32_t at = 0;
+    stack[at++] = 0;
+    while (at > 0) {
+        const rt_bvh_node* node = &sc->bvh_nodes[stack[--at]];
+        if (!ray_intersect_bv(ray, node->bv_p, node->bv_r, *t)) continue;
+        if (node->count) {
+            for (uint32_t li = 0; li < node->count; ++li) {
+                const uint32_t pi = sc->bvh_indices[node->left_first + li];
+                if (pi == ignored) continue;
+                const rt_primitive* prim = &sc->primitives[pi];
+                Ray ir = transform_ray(ray, &sc->transforms[prim->transform_index].inverse);
+                int hit = 0;
+                if (prim->type == RT_PRIMITIVE_SPHERE) hit = ray_intersect_sphere(&ir, prim->p[0], t);
+                else if (prim->type == RT_PRIMITIVE_BOX) hit = ray_intersect_box(&ir, v3(prim->p[0], prim->p[1], prim->p[2]), t);
+                else if (prim->type == RT_PRIMITIVE_MESH) {
+                    if (list || calls) g[GW_CALLS]++;
+                    if (list) {
+                        const rt_bvh_node* root = &sc->meshes[prim->mesh_index].nodes[0];
+                        if (ray_intersect_bv(&ir, root->bv_p, root->bv_r, *t)) {
+                            if (*n < 64) list[*n] = pi;
+                            ++*n;
+                        }
+                    } else {
+                        hit = gw_mesh(sc, prim, ray, occ, t, g);
+                    }
+                }
+                if (hit && occ) return 1;
+            }
+        } else {
+            const uint32_t left = node->left_first;
+            if (at + 2 > 64) break;
+            if (neg[node->split_axis]) { stack[at++] = left; stack[at++] = left + 1; }
+            else { stack[at++] = left + 1; stack[at++] = left; }
+        }
+    }
+    return 0;
+}
+
+static void gpu_walk_query(const rt_scene_desc* sc, const Ray* ray, int occ, uint32_t ignored, uint64_t* g) {
+    float t = ray->max_t;
+    for (uint32_t i = 0; i < sc->plane_count; ++i) {                  /* the planes first */
+        const rt_primitive* pl = &sc->planes[i];
+        if (ray_intersect_plane(ray, v3(pl->p[0], pl->p[1], pl->p[2]), pl->p[3], &t) && occ) return;
+    }
+    if (!sc->bvh_node_count) return;
+    /* the prologue walks the top level when it fits its tables (top_sequences, rt_kernels.hip) */
+    if (g_gw_top && sc->bvh_node_count <= 255 && sc->bvh_index_count <= 63) {
+        static const int oct0[3] = {0, 0, 0};
+        uint32_t list[64], n = 0;
+        if (gw_top(sc, ray, oct0, occ, ignored, &t, list, &n, g, 0)) return;
+        if (n == 0) return;                                            /* not queued */
+        if (n <= g_gw_mlist) {
+            for (uint32_t k = 0; k < n; ++k)
+                if (gw_mesh(sc, &sc->primitives[list[k]], ray, occ, &t, g) && occ) return;
+            return;
+        }
+        (void)gw_top(sc, ray, ray->neg, occ, ignored, &t, NULL, NULL, g, 0);   /* MLIST_FULL: the kernel walks */
+        return;
+    }
+    const rt_bvh_node* root = &sc->bvh_nodes[0];
+    if (!ray_intersect_bv(ray, root->bv_p, root->bv_r, t)) return;
+    (void)gw_top(sc, ray, ray->neg, occ, ignored, &t, NULL, NULL, g, 1);      /* the kernel's walk reaches them */
+}
+
 /* ====================================================================== */
 /* Integrator (RT/integrators.cpp)                                        */
 /* ====================================================================== */
@@ -675,6 +826,8 @@ typedef struct {
     const rt_material* air;
     uint64_t closest_rays, shadow_rays;
     const EnvTab* env;    /* NULL: the reference's estimator */
+    uint64_t ts[2][TS_N]; /* TraversalStats per query kind: [0] intersect_scene, [1] intersect_shadow_ray */
+    uint64_t gw[2][GW_N]; /* the GPU walk's counts (gpu_walk_query), when g_gw_on */
 } Ctx;
 
 static int g_env_sampling = 0;
@@ -949,7 +1102,8 @@ static V3 advanced_integrator(Ctx* ctx, Sampler* sampler, RandomSeries* entropy,
     for (uint32_t bounce = 0; bounce < st->max_bounce_count; ++bounce) {
         Hit h;
         ctx->closest_rays++;
-        intersect_scene_internal(scene, &ray, 0, 0, &h);
+        intersect_scene_internal(scene, &ray, 0, 0, &h, ctx->ts[0]);
+        if (g_gw_on) gpu_walk_query(scene, &ray, 0, 0, ctx->gw[0]);
         V3 N = h.n, I = h.hit_p;
         float t = h.t;
         if (h.hit) {
@@ -1043,7 +1197,8 @@ static V3 advanced_integrator(Ctx* ctx, Sampler* sampler, RandomSeries* entropy,
                                         Hit sh;
                                         Ray sray = make_ray(add(I, muls(L, EPSILON)), L, FLT_MAX);
                                         ctx->shadow_rays++;
-                                        if (!intersect_scene_internal(scene, &sray, 1, 0, &sh)) {
+                                        if (g_gw_on) gpu_walk_query(scene, &sray, 1, 0, ctx->gw[1]);
+                                        if (!intersect_scene_internal(scene, &sray, 1, 0, &sh, ctx->ts[1])) {
                                             float bpdf = (st->importance_sample_diffuse ? ndl / PI_32
                                                                                         : 1.0f / (2.0f*PI_32));
                                             float pdf = st->use_mis ? q*pe + bpdf : q*pe;
@@ -1062,7 +1217,8 @@ static V3 advanced_integrator(Ctx* ctx, Sampler* sampler, RandomSeries* entropy,
                                     Hit sh;
                                     Ray sray = make_ray(add(I, muls(L, EPSILON)), L, ls.dist - 2*EPSILON);
                                     ctx->shadow_rays++;
-                                    if (!intersect_scene_internal(scene, &sray, 1, lid, &sh)) {
+                                    if (g_gw_on) gpu_walk_query(scene, &sray, 1, lid, ctx->gw[1]);
+                                    if (!intersect_scene_internal(scene, &sray, 1, lid, &sh, ctx->ts[1])) {
                                         float sa = (nndl * ls.A) / ls.dist_sq;
                                         float pdf;
                                         if (st->use_mis) {
@@ -1280,6 +1436,7 @@ typedef struct {
     float** tile_bufs;            /* per listed tile window buffers (threads > 1) */
     atomic_uint next;
     atomic_ullong closest, shadow;
+    atomic_ullong ts[2][TS_N];
     rt_material air;
     const EnvTab* env;
 } Job;
@@ -1299,7 +1456,9 @@ static void tile_window(const Job* J, uint32_t tile, int64_t* wx0, int64_t* wy0,
 }
 
 static void render_tile(Job* J, uint32_t tile, float* win, int64_t wx0, int64_t wy0, int64_t ww) {
-    Ctx ctx = { J->scene, J->settings, &J->air, 0, 0, J->env };
+    Ctx ctx;
+    memset(&ctx, 0, sizeof(ctx));
+    ctx.scene = J->scene; ctx.settings = J->settings; ctx.air = &J->air; ctx.env = J->env;
     const rt_settings* st = J->settings;
     uint32_t min_x = J->tile_w*(tile % J->tcx), min_y = J->tile_h*(tile / J->tcx);
     uint32_t max_x = min_x + J->tile_w < J->w ? min_x + J->tile_w : J->w;
@@ -1335,6 +1494,9 @@ static void render_tile(Job* J, uint32_t tile, float* win, int64_t wx0, int64_t 
     }
     atomic_fetch_add(&J->closest, ctx.closest_rays);
     atomic_fetch_add(&J->shadow, ctx.shadow_rays);
+    for (int k = 0; k < 2; ++k)
+        for (int i = 0; i < TS_N; ++i) atomic_fetch_add(&J->ts[k][i], ctx.ts[k][i]);
+    gw_add(ctx.gw);
 }
 
 static void* worker(void* arg) {
@@ -1370,6 +1532,17 @@ static int validate(const rt_scene_desc* scene, const rt_settings* st, const rt_
     return RT_OK;
 }
 
+/* rt_stats::traversal from the reference's counts (the reference's own TraversalStats, per kind) */
+static void set_traversal(rt_stats* stats, const uint64_t ts[2][TS_N]) {
+    for (int k = 0; k < 2; ++k) {
+        stats->traversal[k].mesh_intersection_count = ts[k][TS_CALLS];
+        stats->traversal[k].mesh_bvh_traversals = ts[k][TS_BVH];
+        stats->traversal[k].mesh_node_traversals = ts[k][TS_NODES];
+        stats->traversal[k].mesh_leaf_traversals = ts[k][TS_LEAVES];
+        stats->trace_steps[k] = 0;
+    }
+}
+
 static void init_air(rt_material* air) {        /* `Material air` RT/integrators.cpp:597-599 */
     memset(air, 0, sizeof(*air));
     air->ior = 1.0f;
@@ -1398,6 +1571,8 @@ int oracle_render_tiles(const rt_scene_desc* scene, const rt_camera* camera, con
     atomic_init(&J->next, 0u);
     atomic_init(&J->closest, 0ull);
     atomic_init(&J->shadow, 0ull);
+    for (int k = 0; k < 2; ++k)
+        for (int i = 0; i < TS_N; ++i) atomic_init(&J->ts[k][i], 0ull);
     if (threads <= 1) {
         J->direct = accum->pixels;
         worker(J);
@@ -1436,6 +1611,10 @@ int oracle_render_tiles(const rt_scene_desc* scene, const rt_camera* camera, con
         stats->samples = samples;
         stats->iterations = 0;
         stats->seconds = now_s() - t0;
+        uint64_t ts[2][TS_N];
+        for (int k = 0; k < 2; ++k)
+            for (int i = 0; i < TS_N; ++i) ts[k][i] = atomic_load(&J->ts[k][i]);
+        set_traversal(stats, ts);
     }
     if (have_env) env_tab_free(&env);
     free(J);
@@ -1476,7 +1655,9 @@ int oracle_trace_samples(const rt_scene_desc* scene, const rt_camera* camera, co
     init_air(&air);
     EnvTab env;
     const int have_env = g_env_sampling && settings->next_event_estimation && env_tab_build(scene, &env);
-    Ctx ctx = { scene, settings, &air, 0, 0, have_env ? &env : NULL };
+    Ctx ctx;
+    memset(&ctx, 0, sizeof(ctx));
+    ctx.scene = scene; ctx.settings = settings; ctx.air = &air; ctx.env = have_env ? &env : NULL;
     CamSetup c = cam_setup(camera, w, h);
     uint32_t tcx = (w + tile_w - 1) / tile_w;
     for (uint32_t i = 0; i < count; ++i) {
@@ -1499,7 +1680,9 @@ int oracle_trace_samples(const rt_scene_desc* scene, const rt_camera* camera, co
         stats->samples = count;
         stats->iterations = 0;
         stats->seconds = 0;
+        set_traversal(stats, ctx.ts);
     }
+    gw_add(ctx.gw);
     return RT_OK;
 }
 
@@ -1509,7 +1692,7 @@ int oracle_debug_intersect(const rt_scene_desc* scene, uint32_t count, const rt_
         Ray r = make_ray(rays[i].o, rays[i].d, rays[i].max_t);
         Hit h;
         memset(&h, 0, sizeof(h));
-        int hit = intersect_scene_internal(scene, &r, occlusion, rays[i].ignored_primitive, &h);
+        int hit = intersect_scene_internal(scene, &r, occlusion, rays[i].ignored_primitive, &h, NULL);
         rt_hit_record* o = &out[i];
         memset(o, 0, sizeof(*o));
         o->t = h.t;

@@ -88,6 +88,15 @@ float    oracle_asinf(float x);
 void     oracle_set_math_mode(int libm);
 /* 1 = environment-map sampling in the NEE, as rt_set_env_sampling (include/rt_abi.h); 0 = off */
 void     oracle_set_env_sampling(int mode);
+/* rt_stats::traversal of the oracle's renders is the reference's own TraversalStats (BVH2 pops,
+ * its front-to-back walk; RT/intersection.cpp:254, :378-380).  The GPU library counts its own walk
+ * (rt_abi.h).  oracle_gpu_walk_stats(1, ...) additionally restates that walk in every query of the
+ * following renders (the prologue's order, mlist_max = RT_MLIST_MAX of the GPU run, top_prologue = 0
+ * as RT_TOP_PROLOGUE=0) and resets the sums; oracle_gpu_walk_result gives them per kind (closest-hit,
+ * then shadow): mesh instances reached (the GPU's mesh_intersection_count), mesh instances entered by
+ * the trace kernels, leaves entered (the GPU's mesh_leaf_traversals). */
+void     oracle_gpu_walk_stats(int on, uint32_t mlist_max, int top_prologue);
+void     oracle_gpu_walk_result(uint64_t out[6]);
 /* Mitchell–Netravali and friends (RT/reconstruction_filters.cpp:8-95) + LUT */
 int      oracle_load_filter(const char* name, rt_filter_cache* out);
 

@@ -117,6 +117,16 @@ int main(int argc, char** argv) {
     fwrite(bgra, sizeof(uint32_t), (size_t)w*h, f);
     fwrite(&stats.closest_hit_rays, sizeof(uint64_t), 1, f);
     fwrite(&stats.shadow_rays, sizeof(uint64_t), 1, f);
+    /* render_all_tiles' out_stats (RT/raytracer.cpp:727-730): the reference's TraversalStats are the
+       sums of the two query kinds */
+    {
+        const rt_traversal_stats* k = stats.traversal;
+        const uint64_t t[4] = {k[0].mesh_intersection_count + k[1].mesh_intersection_count,
+                               k[0].mesh_bvh_traversals + k[1].mesh_bvh_traversals,
+                               k[0].mesh_node_traversals + k[1].mesh_node_traversals,
+                               k[0].mesh_leaf_traversals + k[1].mesh_leaf_traversals};
+        fwrite(t, sizeof(uint64_t), 4, f);
+    }
     fclose(f);
     printf("c_host: %ux%u, %llu samples, %llu + %llu rays\n", w, h, (unsigned long long)stats.samples,
            (unsigned long long)stats.closest_hit_rays, (unsigned long long)stats.shadow_rays);

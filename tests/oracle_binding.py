@@ -55,6 +55,8 @@ def load():
         "oracle_set_env_sampling": (None, [C.c_int]),
         "oracle_load_filter": (C.c_int, [C.c_char_p, P(abi.FilterCache)]),
         "oracle_postprocess": (None, [P(abi.AccumulationBuffer), P(abi.PostSettings), C.c_uint32, P(C.c_uint32)]),
+        "oracle_gpu_walk_stats": (None, [C.c_int, C.c_uint32, C.c_int]),
+        "oracle_gpu_walk_result": (None, [P(C.c_uint64)]),
     }
     for name, (res, args) in fns.items():
         f = getattr(lib, name)
@@ -133,4 +135,27 @@ class env_sampling:
 
     def __exit__(self, *exc):
         load().oracle_set_env_sampling(0)
+        return False
+
+
+class gpu_walk:
+    """with gpu_walk() as g: the oracle's renders also restate the GPU library's own traversal walk
+    (oracle_gpu_walk_stats); afterwards g.result = {"calls": [closest, shadow], "entries": [...],
+    "leaves": [...]}: the GPU's rt_stats::traversal mesh_intersection_count, the mesh instances its
+    trace kernels enter, and its mesh_leaf_traversals for the same queries."""
+
+    def __init__(self, mlist_max=4, top_prologue=True):
+        self.mlist_max, self.top = mlist_max, top_prologue
+        self.result = None
+
+    def __enter__(self):
+        load().oracle_gpu_walk_stats(1, self.mlist_max, int(self.top))
+        return self
+
+    def __exit__(self, *exc):
+        out = (C.c_uint64 * 6)()
+        load().oracle_gpu_walk_result(out)
+        load().oracle_gpu_walk_stats(0, 4, 1)
+        self.result = {"calls": [int(out[0]), int(out[3])], "entries": [int(out[1]), int(out[4])],
+                       "leaves": [int(out[2]), int(out[5])]}
         return False

@@ -24,7 +24,7 @@ def test_every_declared_symbol_is_exported(rt):
     assert len(names) > 40
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.rt_abi_version() == 5
+    assert lib.rt_abi_version() == 6
 
 
 def test_ctypes_table_covers_header(rt):
@@ -39,6 +39,26 @@ def test_struct_sizes_match_reference_layout(rt):
     assert C.sizeof(a.BvhNode) == 32                   # RT/bvh.h:31-37
     assert C.sizeof(a.M4x4Inv) == 128
     assert C.sizeof(a.FilterCache) == 8 + 512 * 4     # RT/Raytracer.h:34-40
+
+
+def test_stats_layout_matches_header(rt, tmp_path):
+    """The ctypes rt_stats (with the TraversalStats fields of ABI v6) has the C header's layout."""
+    import ctypes as C
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("needs gcc")
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt_abi.h"\n'
+                   'int main(void) { printf("%zu %zu %zu %zu\\n", sizeof(rt_stats), offsetof(rt_stats, traversal), '
+                   'offsetof(rt_stats, trace_steps), sizeof(rt_traversal_stats)); return 0; }\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    size, off_trav, off_steps, tsize = map(int, subprocess.check_output([str(exe)]).split())
+    a = rt.abi
+    assert C.sizeof(a.Stats) == size
+    assert a.Stats.traversal.offset == off_trav and a.Stats.trace_steps.offset == off_steps
+    assert C.sizeof(a.TraversalStats) == tsize == 32
 
 
 def test_no_cpu_fallback_without_gpu(rt):

@@ -8,6 +8,11 @@ over gloo (RCCL refuses two ranks on one device), and checks what that flow comp
 * the ray, sample and C4 counts summed over the ranks equal a one-rank run's (the pass shares
   are disjoint and every sample keeps its key);
 * the frame reduced into rank 0 equals the one-rank frame up to float summation order.
+
+The driver's N-GPU runs take the RCCL branch (init_process_group("nccl"), the device-tensor
+reduce of the framebuffer, the cuda all-reduces of the totals).  RCCL refuses two ranks on one
+device, so test_bench_rccl_one_rank runs that branch with one rank (--force-dist) and checks
+that it changes nothing: the same JSON counts and the same frame, bit for bit.
 """
 import json
 import os
@@ -62,3 +67,27 @@ def test_bench_two_ranks_match_one(tmp_path):
     assert two["samples_per_s"] * two["ms_per_step"] == pytest.approx(one["samples_per_s"] * one["ms_per_step"], rel=1e-3)
     assert (two["c4"]["closest_hit_rays"], two["c4"]["shadow_rays"]) == (one["c4"]["closest_hit_rays"], one["c4"]["shadow_rays"])
     assert err <= 1e-5
+
+
+@pytest.mark.gpu
+def test_bench_rccl_one_rank(tmp_path):
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    plain = _run([sys.executable, "bench.py", "--gpus", "1"] + ARGS + ["--dump-frame", str(tmp_path / "plain.npy")], env)
+    rccl = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "1",
+                 "--dist-backend", "nccl", "--force-dist"] + ARGS + ["--dump-frame", str(tmp_path / "rccl.npy")], env)
+    from parity_report import REPORT
+    f1, f2 = np.load(tmp_path / "plain.npy"), np.load(tmp_path / "rccl.npy")
+    REPORT["bench_rccl_one_rank"] = {"frames_bit_identical": bool(np.array_equal(f1, f2)),
+                                     "plain": {k: plain[k] for k in ("value", "ms_per_step")},
+                                     "rccl": {k: rccl[k] for k in ("value", "ms_per_step")},
+                                     "parallelism": rccl["config"]["parallelism"]}
+    assert rccl["config"]["parallelism"] == "passes%1+rccl_reduce"
+    assert rccl["n_gpus"] == plain["n_gpus"] == 1
+    for k in ("closest_hit_rays", "shadow_rays", "traced_rays", "traversal_stats"):
+        assert rccl[k] == plain[k], k
+    assert (rccl["c4"]["closest_hit_rays"], rccl["c4"]["shadow_rays"]) == (plain["c4"]["closest_hit_rays"],
+                                                                           plain["c4"]["shadow_rays"])
+    assert np.array_equal(f1, f2)

@@ -41,9 +41,12 @@ def test_c_host_frame_and_picture(rt, tmp_path):
     acc = np.frombuffer(raw, np.float32, count=w * h * 4).reshape(h, w, 4)
     pic = np.frombuffer(raw, np.uint32, count=w * h, offset=16 * w * h).reshape(h, w)
     rays = np.frombuffer(raw, np.uint64, count=2, offset=20 * w * h)
+    trav = np.frombuffer(raw, np.uint64, count=4, offset=20 * w * h + 16)
     scene, cam, st, fc, post = rt.load_preset("c1", w, h)
     cpu, cs = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1)
     assert (int(rays[0]), int(rays[1])) == (cs.closest_hit_rays, cs.shadow_rays)
+    # TraversalStats through the C ABI: C1 has no mesh, so both walks count nothing
+    assert trav.tolist() == [0, 0, 0, 0] == list(cs.traversal_total().values())
     assert np.array_equal(acc, cpu)
     ref_pic = ob.postprocess(cpu, post, total_frame_index=1)
     assert np.array_equal(pic, ref_pic)

@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++")
 def test_sincos_matches_separate_calls(tmp_path):
     exe = str(tmp_path / "check_sincos")
-    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-DRT_DMATH_HOST_TEST", "-DRT_RCP_CR=0",
+    subprocess.check_call(["g++", "-O2", "-ffp-contract=off", "-DRT_DMATH_HOST_TEST",
                            "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
                            os.path.join(ROOT, "tools", "check_sincos.cpp"), "-o", exe])
     out = subprocess.run([exe, "97"], capture_output=True, text=True, timeout=300)

@@ -8,9 +8,15 @@ reference-order splat, RT/raytracer.cpp:366-495, :692-757):
 * C3 (1920x1080, 256 spp) and C4 (1920x1080, 256 spp, ~250k triangles): the whole frame, rel L2
   <= 1e-5 (the streaming splat sums a pixel pass by pass, the reference tile by tile) and the same
   closest-hit and shadow ray counts, call for call;
-* C5 (3840x2160, 1024 spp, blue noise): the GPU renders the whole frame; the oracle renders an
-  evenly spaced subset of its 64x64 tiles (oracle_render_tiles), compared on the pixels whose
-  whole filter window lies in a rendered tile (at least kernel_size px inside it).
+* the frame's TraversalStats (rt_stats::traversal, RT/intersection.h:33-40): the GPU counts its own
+  walk (include/rt_abi.h), so its mesh_intersection_count must equal, query kind by query kind, the
+  oracle's restatement of that walk (oracle_gpu_walk_stats), and its leaves entered must agree with
+  the restatement's (which leaves out the GPU's pruning for rays with an exactly-zero direction
+  component); the reference's own counts from the same render (BVH2 pops, front-to-back order) are
+  reported beside them;
+* C5 (3840x2160, 1024 spp, blue noise): the GPU renders the tiles t % 85 == 42 of the frame
+  (RT_SHARD_TILES, shard 42 of 85: 24 tiles spread over the frame) and the oracle the same tiles:
+  every pixel, filter halos included, rel L2 <= 1e-5, and identical ray counts.
 
 The oracle runs on the box's cores (bench.host_cores, 16 on a one-GPU box): ~30 s for C3.
 """
@@ -53,51 +59,84 @@ def test_full_frame_default_path(rt, preset):
         dev.close()
     assert gs.splat_mode == rt.abi.RT_SPLAT_STREAM
     threads = _threads()
-    cpu, cs = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=threads)
+    with ob.gpu_walk() as walk:
+        cpu, cs = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=threads)
     err = rel_l2(gpu, cpu)
+    trav = traversal_report(gs, cs, walk.result)
     REPORT[f"fullscale_{preset}_1080p_256spp"] = {
         "rel_l2": err, "max_abs_weight_diff": float(np.abs(gpu[..., 3] - cpu[..., 3]).max()),
         "gpu_rays": [int(gs.closest_hit_rays), int(gs.shadow_rays)], "oracle_rays": [int(cs.closest_hit_rays), int(cs.shadow_rays)],
         "samples": int(gs.samples), "iterations": int(gs.iterations), "oracle_threads": threads,
-        "gpu_seconds": gs.seconds}
+        "gpu_seconds": gs.seconds, "traversal": trav}
     assert gs.samples == cs.samples == w * h * 256
     assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
-    assert np.isfinite(gpu).all() == np.isfinite(cpu).all()
+    assert np.isfinite(gpu).all() and np.isfinite(cpu).all()
     assert err <= 1e-5
+    check_traversal(gs, walk.result)
 
 
-def test_c5_tile_subset(rt):
+def traversal_report(gs, cs, walk):
+    """The frame's TraversalStats: the GPU's (its walk, BVH4 units), the oracle's restatement of that
+    walk, and the reference's own counts (BVH2 pops in its front-to-back walk)."""
+    out = {}
+    for k, kind in enumerate(("closest", "shadow")):
+        g = gs.traversal[k].as_dict()
+        g["trace_steps"] = int(gs.trace_steps[k])
+        out[kind] = {"gpu": g,
+                     "gpu_walk_restated": {"mesh_intersection_count": walk["calls"][k],
+                                           "instances_entered": walk["entries"][k],
+                                           "mesh_leaf_traversals": walk["leaves"][k]},
+                     "reference_walk": cs.traversal[k].as_dict()}
+    return out
+
+
+def check_traversal(gs, walk):
+    for k in range(2):
+        t = gs.traversal[k]
+        # the instances the walk reaches: exact, query kind by query kind
+        assert t.mesh_intersection_count == walk["calls"][k], (k, t.mesh_intersection_count, walk["calls"][k])
+        # leaves entered: the restatement walks every node the GPU's pruned walk can skip
+        assert t.mesh_leaf_traversals <= walk["leaves"][k]
+        assert t.mesh_leaf_traversals >= walk["leaves"][k] * (1 - 1e-4), (k, t.mesh_leaf_traversals, walk["leaves"][k])
+        # a BVH4 step is an instance's entry, an interior node or up to two triangles of a leaf
+        assert t.mesh_bvh_traversals >= t.mesh_node_traversals + t.mesh_leaf_traversals
+        assert gs.trace_steps[k] >= t.mesh_bvh_traversals
+
+
+def test_c5_tile_shard_exact(rt):
+    """C5 at 4K, 1024 spp: shard 42 of 85 by tiles (the tiles t % 85 == 42: 24 tiles evenly spread
+    over the 60 x 34 tile frame) on the GPU against the same tiles in the oracle."""
     w, h = 3840, 2160
     scene, cam, st, fc, post = rt.load_preset("c5", w, h)
     assert st.samples_per_pixel == 1024
+    tcx, tcy = (w + 63) // 64, (h + 63) // 64
+    count, index = 85, 42
+    tiles = [t for t in range(tcx * tcy - 1, -1, -1) if t % count == index]    # the reference's queue order
+    assert len(tiles) == 24
     dev = rt.DeviceScene(scene, 0)
     try:
-        gpu, gs = dev.render(cam, st, fc, w, h)
+        with dev.configured(shard_mode=rt.abi.RT_SHARD_TILES):
+            gpu, gs = dev.render(cam, st, fc, w, h, shard_index=index, shard_count=count)
     finally:
         dev.close()
-    tcx, tcy = (w + 63) // 64, (h + 63) // 64
-    n_tiles = 24
-    step = tcx * tcy // n_tiles
-    tiles = [k * step + step // 2 for k in range(n_tiles)]
     lib = ob.load()
     cpu = np.zeros((h, w, 4), np.float32)
     buf = rt.abi.AccumulationBuffer(w, h, 0, cpu.ctypes.data_as(C.POINTER(C.c_float)))
     arr = (C.c_uint32 * len(tiles))(*tiles)
     cs = rt.abi.Stats()
-    assert lib.oracle_render_tiles(C.byref(scene.desc()), C.byref(cam), C.byref(st), C.byref(fc), 64, 64, 0, 0,
-                                   _threads(), len(tiles), arr, C.byref(buf), C.byref(cs)) == 0
-    ks = int(fc.kernel_size)
-    mask = np.zeros((h, w), bool)
-    for t in tiles:
-        x0, y0 = (t % tcx) * 64, (t // tcx) * 64
-        x1, y1 = min(x0 + 64, w), min(y0 + 64, h)
-        mask[y0 + ks:y1 - ks, x0 + ks:x1 - ks] = True
-    err = rel_l2(gpu[mask], cpu[mask])
-    REPORT["fullscale_c5_4k_1024spp_tiles"] = {"rel_l2": err, "tiles": tiles, "pixels_compared": int(mask.sum()),
-                                               "kernel_size": ks, "gpu_rays": [int(gs.closest_hit_rays), int(gs.shadow_rays)],
-                                               "oracle_rays_subset": [int(cs.closest_hit_rays), int(cs.shadow_rays)],
-                                               "gpu_seconds": gs.seconds, "iterations": int(gs.iterations)}
-    assert gs.samples == w * h * 1024
-    assert mask.sum() >= n_tiles * (64 - 2 * ks) ** 2 // 2
-    assert np.isfinite(gpu).all()
+    with ob.gpu_walk() as walk:
+        assert lib.oracle_render_tiles(C.byref(scene.desc()), C.byref(cam), C.byref(st), C.byref(fc), 64, 64, 0, 0,
+                                       _threads(), len(tiles), arr, C.byref(buf), C.byref(cs)) == 0
+    err = rel_l2(gpu, cpu)
+    touched = int((cpu[..., 3] != 0).sum())
+    REPORT["fullscale_c5_4k_1024spp_shard42of85"] = {
+        "rel_l2_every_pixel": err, "tiles": tiles, "pixels_with_weight": touched,
+        "gpu_rays": [int(gs.closest_hit_rays), int(gs.shadow_rays)], "oracle_rays": [int(cs.closest_hit_rays), int(cs.shadow_rays)],
+        "samples": int(gs.samples), "gpu_seconds": gs.seconds, "iterations": int(gs.iterations),
+        "traversal": traversal_report(gs, cs, walk.result)}
+    assert gs.samples == cs.samples == 24 * 64 * 64 * 1024
+    assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
+    assert np.isfinite(gpu).all() and np.isfinite(cpu).all()
+    assert touched > 24 * 64 * 64
     assert err <= 1e-5
+    check_traversal(gs, walk.result)

@@ -316,13 +316,14 @@ def test_postprocess_bit_exact(c1, frame):
     REPORT[f"postprocess_frame{frame}"] = {"pixels_bit_identical": same}
 
 
-@pytest.mark.parametrize("env", [{"RT_TOP_PROLOGUE": "0"}, {"RT_MLIST_MAX": "1"}, {"RT_MLIST_MAX": "0"}])
+@pytest.mark.parametrize("env", [{}, {"RT_TOP_PROLOGUE": "0"}, {"RT_MLIST_MAX": "1"}, {"RT_MLIST_MAX": "0"}])
 def test_top_level_paths(rt, env, monkeypatch):
     """The three ways a queued ray meets the top level (ray prologue):
     the trace kernel walks all of it (RT_TOP_PROLOGUE=0), the prologue tests the
     analytic primitives and the kernel re-walks everything because the mesh list
     overflowed (RT_MLIST_MAX=1 on C4's four instances, and 0), or the default mesh
-    list (the other tests).  Per-sample results stay bit-exact against the oracle."""
+    list.  Per-sample results stay bit-exact against the oracle, and the TraversalStats
+    (rt_stats::traversal) are those of the oracle's restatement of each walk."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     scene, cam, st, fc, post = rt.load_preset("c4", 192, 108)
@@ -333,11 +334,20 @@ def test_top_level_paths(rt, env, monkeypatch):
         gpu, gstats = dev.trace_samples(cam, st, 192, 108, xy, s)
     finally:
         dev.close()
-    cpu, cstats = ob.trace_samples(scene.desc(), cam, st, 192, 108, xy, s)
+    with ob.gpu_walk(mlist_max=int(env.get("RT_MLIST_MAX", 4)), top_prologue=env.get("RT_TOP_PROLOGUE") != "0") as walk:
+        cpu, cstats = ob.trace_samples(scene.desc(), cam, st, 192, 108, xy, s)
     same = np.all((gpu == cpu) | (np.isnan(gpu) & np.isnan(cpu)), axis=1).mean()
-    REPORT["top_level_" + "_".join(f"{k}={v}" for k, v in env.items())] = {"bit_exact_fraction": float(same)}
+    calls = [int(gstats.traversal[k].mesh_intersection_count) for k in range(2)]
+    leaves = [int(gstats.traversal[k].mesh_leaf_traversals) for k in range(2)]
+    REPORT["top_level_" + ("_".join(f"{k}={v}" for k, v in env.items()) or "default")] = {
+        "bit_exact_fraction": float(same), "gpu_calls": calls, "restated_calls": walk.result["calls"],
+        "gpu_leaves": leaves, "restated_leaves": walk.result["leaves"],
+        "reference_walk_calls": [int(cstats.traversal[k].mesh_intersection_count) for k in range(2)]}
     assert same >= 0.999
     assert gstats.closest_hit_rays == cstats.closest_hit_rays or same < 1.0
+    assert calls == walk.result["calls"]
+    for k in range(2):
+        assert walk.result["leaves"][k] * (1 - 1e-3) <= leaves[k] <= walk.result["leaves"][k]
 
 
 @pytest.mark.parametrize("how", ["budget", "mode"])
