@@ -295,3 +295,15 @@ def test_scene_config_is_per_scene(rt, monkeypatch):
         a.close()
         if b is not None:
             b.close()
+
+
+@pytest.mark.parametrize("var,value", [("RT_SPLAT", "exact"), ("RT_SPLAT", "3"), ("RT_PARTITIONS", "9"),
+                                       ("RT_FUSE_PATHS", "-1"), ("RT_SAMPLE_BUDGET_GB", "lots")])
+def test_bad_override_rejected(rt, monkeypatch, var, value):
+    """A malformed test-override variable fails rt_scene_upload with RT_ERROR_INVALID naming it,
+    instead of silently becoming 0 (RT_SPLAT=exact read as RT_SPLAT_STREAM)."""
+    scene, cam, st, fc, post = rt.load_preset("c1", 32, 32)
+    monkeypatch.setenv(var, value)
+    with pytest.raises(rt.RenderError) as e:
+        rt.DeviceScene(scene, 0)
+    assert e.value.code == rt.abi.RT_ERROR_INVALID and var in str(e.value)
