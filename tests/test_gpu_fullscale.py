@@ -95,9 +95,11 @@ def check_traversal(gs, walk):
         t = gs.traversal[k]
         # the instances the walk reaches: exact, query kind by query kind
         assert t.mesh_intersection_count == walk["calls"][k], (k, t.mesh_intersection_count, walk["calls"][k])
-        # leaves entered: the restatement walks every node the GPU's pruned walk can skip
+        # leaves entered: the restatement enters every leaf whose box the ray crosses before the hit it
+        # ends with; the GPU's BVH4 walk skips the ones it culls against a closer hit found earlier in
+        # its own child order (measured: 4e-4 fewer on C3 and C4), so a bound, not an identity
         assert t.mesh_leaf_traversals <= walk["leaves"][k]
-        assert t.mesh_leaf_traversals >= walk["leaves"][k] * (1 - 1e-4), (k, t.mesh_leaf_traversals, walk["leaves"][k])
+        assert t.mesh_leaf_traversals >= walk["leaves"][k] * (1 - 1e-3), (k, t.mesh_leaf_traversals, walk["leaves"][k])
         # a BVH4 step is an instance's entry, an interior node or up to two triangles of a leaf
         assert t.mesh_bvh_traversals >= t.mesh_node_traversals + t.mesh_leaf_traversals
         assert gs.trace_steps[k] >= t.mesh_bvh_traversals
@@ -134,7 +136,8 @@ def test_c5_tile_shard_exact(rt):
         "gpu_rays": [int(gs.closest_hit_rays), int(gs.shadow_rays)], "oracle_rays": [int(cs.closest_hit_rays), int(cs.shadow_rays)],
         "samples": int(gs.samples), "gpu_seconds": gs.seconds, "iterations": int(gs.iterations),
         "traversal": traversal_report(gs, cs, walk.result)}
-    assert gs.samples == cs.samples == 24 * 64 * 64 * 1024
+    area = sum((min(64, w - (t % tcx)*64)) * (min(64, h - (t // tcx)*64)) for t in tiles)   # bottom-row tiles: 48 rows
+    assert gs.samples == cs.samples == area * 1024
     assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
     assert np.isfinite(gpu).all() and np.isfinite(cpu).all()
     assert touched > 24 * 64 * 64

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 tag=${TAG:-r04a}
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 \
+  timeout -k 10 ${PYTEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 170 \
       --timeout-method thread ${PYTEST_ARGS} > gpurun_out/${tag}_pytest.log 2>&1
   rc=$?
   echo "pytest rc=$rc"; tail -30 gpurun_out/${tag}_pytest.log
