@@ -95,11 +95,11 @@ def check_traversal(gs, walk):
         t = gs.traversal[k]
         # the instances the walk reaches: exact, query kind by query kind
         assert t.mesh_intersection_count == walk["calls"][k], (k, t.mesh_intersection_count, walk["calls"][k])
-        # leaves entered: the restatement enters every leaf whose box the ray crosses before the hit it
-        # ends with; the GPU's BVH4 walk skips the ones it culls against a closer hit found earlier in
-        # its own child order (measured: 4e-4 fewer on C3 and C4), so a bound, not an identity
-        assert t.mesh_leaf_traversals <= walk["leaves"][k]
-        assert t.mesh_leaf_traversals >= walk["leaves"][k] * (1 - 1e-3), (k, t.mesh_leaf_traversals, walk["leaves"][k])
+        # leaves entered: the restatement walks each BVH in the BVH2's front-to-back order, the GPU in
+        # its BVH4 child order, which finds some hits sooner and culls leaves the restatement still
+        # enters (measured: 4e-4 fewer on C3 and C4, one more shadow leaf of 5.2M on the C5 shard)
+        assert abs(t.mesh_leaf_traversals - walk["leaves"][k]) <= 1e-3 * walk["leaves"][k], \
+            (k, t.mesh_leaf_traversals, walk["leaves"][k])
         # a BVH4 step is an instance's entry, an interior node or up to two triangles of a leaf
         assert t.mesh_bvh_traversals >= t.mesh_node_traversals + t.mesh_leaf_traversals
         assert gs.trace_steps[k] >= t.mesh_bvh_traversals
