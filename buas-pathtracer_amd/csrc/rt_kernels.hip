@@ -3682,24 +3682,31 @@ int check_config(const rt_scene_config* c) {
     return RT_OK;
 }
 
+// An integer override `name` from the environment: true and `out` set when present and a whole
+// number in [lo, hi]; a malformed or out-of-range value sets the error (naming `who` and the
+// variable) and clears `ok`.
+bool env_int(const char* who, const char* name, long long lo, long long hi, long long& out, bool& ok) {
+    const char* e = getenv(name);
+    if (!e) return false;
+    char* end = nullptr;
+    errno = 0;
+    const long long v = strtoll(e, &end, 0);
+    if (!*e || *end || errno || v < lo || v > hi) {
+        set_error(std::string(who) + ": bad " + name + "=" + e);
+        ok = false;
+        return false;
+    }
+    out = v;
+    return true;
+}
+
 // The test-override environment variables, applied once at rt_scene_upload (never per frame).
 // A value that is not a whole number (RT_SPLAT=exact) is an error, not a silent 0: false, with
 // the variable named in the error text.
 bool config_from_env(rt_scene_config& c) {
     bool ok = true;
     auto num = [&](const char* name, long long lo, long long hi, long long& out) {
-        const char* e = getenv(name);
-        if (!e) return false;
-        char* end = nullptr;
-        errno = 0;
-        const long long v = strtoll(e, &end, 0);
-        if (!*e || *end || errno || v < lo || v > hi) {
-            set_error(std::string("rt_scene_upload: bad ") + name + "=" + e);
-            ok = false;
-            return false;
-        }
-        out = v;
-        return true;
+        return env_int("rt_scene_upload", name, lo, hi, out, ok);
     };
     long long v = 0;
     if (num("RT_SPLAT", RT_SPLAT_STREAM, RT_SPLAT_ATOMIC, v)) c.splat_mode = (int32_t)v;
@@ -3836,12 +3843,15 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     }
     if ((err = upload(s, d->bvh_indices, d->bvh_index_count, &ds.bvh_idx))) return fail(err);
     {
-        const char* env = getenv("RT_TOP_PROLOGUE");              // 0: the trace kernels walk the top level
+        bool env_ok = true;
+        long long top = 1, mlist = MLIST_MAX;
+        env_int("rt_scene_upload", "RT_TOP_PROLOGUE", 0, 1, top, env_ok);   // 0: the trace kernels walk the top level
+        env_int("rt_scene_upload", "RT_MLIST_MAX", 0, MLIST_MAX, mlist, env_ok);
+        if (!env_ok) return fail(RT_ERROR_INVALID);
         std::vector<float4> seq;
         uint32_t len = 0;
-        if (!(env && env[0] == '0')) seq = top_sequences(d->bvh_nodes, d->bvh_node_count, d->bvh_index_count, len);
-        ds.top_seq = nullptr; ds.top_seq_len = 0; ds.mlist_max = MLIST_MAX;
-        if (const char* m = getenv("RT_MLIST_MAX")) ds.mlist_max = std::min<uint32_t>(MLIST_MAX, (uint32_t)atoi(m));
+        if (top) seq = top_sequences(d->bvh_nodes, d->bvh_node_count, d->bvh_index_count, len);
+        ds.top_seq = nullptr; ds.top_seq_len = 0; ds.mlist_max = (uint32_t)mlist;
         if (!seq.empty()) {
             if ((err = upload(s, seq.data(), seq.size(), &ds.top_seq))) return fail(err);
             ds.top_seq_len = len;
@@ -4011,9 +4021,12 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         // the prologue reads the top-level sequences and leaf records from HBM through the scalar
         // cache, and the strata table stays in HBM (both read through L2): not copied into LDS
         put(BLOB_MESHES, meshes.data(), meshes.size()*sizeof(DevMesh));
-        const char* env = getenv("RT_LDS_SCENE");               // 0: the kernels read the tables from HBM
+        bool env_ok = true;
+        long long lds_scene = 1;                                 // 0: the kernels read the tables from HBM
+        env_int("rt_scene_upload", "RT_LDS_SCENE", 0, 1, lds_scene, env_ok);
+        if (!env_ok) return fail(RT_ERROR_INVALID);
         ds.blob = nullptr; ds.blob_q = 0;
-        if (blob.size() <= 16*(size_t)LDS_SCENE_Q && !(env && env[0] == '0')) {
+        if (blob.size() <= 16*(size_t)LDS_SCENE_Q && lds_scene) {
             std::vector<float4> q(blob.size() / 16);
             memcpy(q.data(), blob.data(), blob.size());
             if ((err = upload(s, q.data(), q.size(), &ds.blob))) return fail(err);
@@ -4031,15 +4044,17 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         // less room for the other partitions' generate / shade blocks.  C3 A/B, 5 alternating
         // pairs: 75 % +1.5 %, 60 % +0.9 %, 50 % +1.5 % (2 pairs), 150 % -0.8 %.  The spill
         // area is sized from the result.
-        int grid_pct = 75;
-        if (const char* e = getenv("RT_TRACE_GRID_PCT")) grid_pct = std::max(1, atoi(e));
+        bool env_ok = true;
+        long long grid_pct = 75, connect_pct = 25, drain_pct = 100;
+        env_int("rt_scene_upload", "RT_TRACE_GRID_PCT", 1, 1000, grid_pct, env_ok);
+        env_int("rt_scene_upload", "RT_CONNECT_GRID_PCT", 1, 1000, connect_pct, env_ok);
+        env_int("rt_scene_upload", "RT_DRAIN_GRID_PCT", 1, 100, drain_pct, env_ok);
+        if (!env_ok) return fail(RT_ERROR_INVALID);
         const uint32_t full = s->trace_grid;
         s->trace_grid = std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)grid_pct / 100ull));
         // Shadow-ray launches carry a quarter of the extension rays (~0.8 per lane of a 75 % grid):
         // a 25 % grid does them as fast and leaves the registers to the other partitions' kernels
         // (C3: +0.6 %, 2 pairs; 40 / 55 % between).
-        int connect_pct = 25;
-        if (const char* e = getenv("RT_CONNECT_GRID_PCT")) connect_pct = std::max(1, atoi(e));
         s->connect_grid = std::min(s->trace_grid,
                                    std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)connect_pct / 100ull)));
         int drain_cu = 0;     // k_drain holds ~220 VGPRs: 2 waves per SIMD; its grid is what fits at once
@@ -4048,8 +4063,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         // (lanes <= the trace grid's: the spill area is sized for those)
         s->drain_grid = std::min(s->trace_grid*(uint32_t)(TB / DTB), (uint32_t)(prop.multiProcessorCount*drain_cu));
         s->drain_lanes_full = s->drain_grid*DTB;
-        if (const char* e = getenv("RT_DRAIN_GRID_PCT"))
-            s->drain_grid = std::max(1u, (uint32_t)((unsigned long long)s->drain_grid*(unsigned)std::max(1, atoi(e)) / 100ull));
+        s->drain_grid = std::max(1u, (uint32_t)((unsigned long long)s->drain_grid*(unsigned long long)drain_pct / 100ull));
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
