@@ -533,32 +533,44 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
 }
 
 // What the traversal steps fetched, for the TraversalStats counts (rt_stats::traversal): each
-// step adds one of these to its lane's Traversal::acc, 4-bit count fields.  ST_ENTRY a mesh
+// step adds one of these to its lane's Traversal::acc, a count field per kind.  ENTRY a mesh
 // instance's top-level leaf record (its object-space ray and root box test: intersect_mesh
-// entered); ST_NODE a mesh BVH4 interior node; ST_LEAF the first triangles of a mesh leaf (the
-// leaf entered); ST_TRIS any step that fetched triangles; ST_TOP a top-level interior node or a
-// sphere's / box's record.  A lane's fields stay below 16 between two flushes (StepCounts).
-constexpr uint32_t ST_ENTRY = 1u << 0, ST_NODE = 1u << 4, ST_LEAF = 1u << 8, ST_TRIS = 1u << 12, ST_TOP = 1u << 16;
+// entered); NODE a mesh BVH4 interior node; LEAF the first triangles of a mesh leaf (the leaf
+// entered); TRIS any step that fetched triangles; TOP a top-level interior node or a sphere's /
+// box's record (none in a listed-only walk).  Fields of B bits: 8 for the four kinds of a
+// listed-only walk, 6 for the five otherwise.  HI holds each field's top bit: a lane whose field
+// reached half its range is flushed (StepCounts) before it can take another MARGIN steps.
+template <bool LST>
+struct StepField {
+    static constexpr uint32_t B = LST ? 8 : 6, M = (1u << B) - 1u;
+    static constexpr uint32_t ENTRY = 1u, NODE = 1u << B, LEAF = 1u << 2*B, TRIS = 1u << 3*B,
+                              TOP = LST ? 0u : 1u << 4*B;
+    static constexpr uint32_t H = 1u << (B - 1);
+    static constexpr uint32_t HI = H | H << B | H << 2*B | H << 3*B | (LST ? 0u : H << 4*B);
+    static constexpr uint32_t MARGIN = (1u << (B - 1)) - 1u;     // steps a lane may take between checks
+};
 
 // TraversalStats counters of a partition: per ray kind (0 closest, 1 shadow) and shard, TV_* counts.
 enum { TV_ENTRIES, TV_NODES, TV_LEAVES, TV_TRIS, TV_TOP, TV_CALLS, TV_N = 8 };
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
-// A wave's step counts.  flush, at a point every lane of the wave reaches, sums the lanes' `acc`
-// (taken from Traversal::acc: 4-bit fields, at most 15 steps per lane since the last flush) over the
-// wave with DPP reductions into the wave's totals, which stay in SGPRs; commit: one lane adds the
-// totals to the partition's counters.
+// A wave's step counts.  flush(acc), at a point every lane of the wave reaches, sums the lanes'
+// Traversal::acc (StepField) over the wave with DPP reductions, two fields per reduction (64 x 255
+// fits 16 bits), into the wave's totals, which stay in SGPRs, and clears it; check(acc) flushes
+// once some lane has a field at half its range; commit: one lane adds the totals to the counters.
 template <bool LST>
 struct StepCounts {
-    uint32_t acc = 0;
+    using F = StepField<LST>;
     uint32_t tot[5] = {0, 0, 0, 0, 0};                 // TV_ENTRIES .. TV_TOP
-    RT_D void flush() {
-        const uint32_t a = __ockl_wfred_add_u32((acc & 0xFu) | ((acc & 0xF0u) << 12));          // entries | nodes
-        const uint32_t b = __ockl_wfred_add_u32(((acc >> 8) & 0xFu) | ((acc & 0xF000u) << 4));  // leaves | tris
+    RT_D void flush(uint32_t& acc) {
+        constexpr uint32_t B = F::B, M = F::M;
+        const uint32_t a = __ockl_wfred_add_u32((acc & M) | (((acc >> B) & M) << 16));              // entries | nodes
+        const uint32_t b = __ockl_wfred_add_u32(((acc >> 2*B) & M) | (((acc >> 3*B) & M) << 16));  // leaves | tris
         tot[TV_ENTRIES] += a & 0xFFFFu; tot[TV_NODES] += a >> 16;
         tot[TV_LEAVES] += b & 0xFFFFu; tot[TV_TRIS] += b >> 16;
-        if (!LST) tot[TV_TOP] += __ockl_wfred_add_u32((acc >> 16) & 0xFu);
+        if (!LST) tot[TV_TOP] += __ockl_wfred_add_u32(acc >> 4*B);
         acc = 0;
     }
+    RT_D void check(uint32_t& acc) { if (__ballot((acc & F::HI) != 0u)) flush(acc); }
     RT_D void commit(unsigned long long* trav, int kind) const {
         if (__lane_id() != (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) return;
 #pragma unroll
@@ -705,11 +717,12 @@ struct Traversal {
     }
 
     // One traversal step; returns false once the query is finished (mode == TM_DONE).  What the
-    // step fetched is added to `acc` (ST_*, the lane's TraversalStats counts since the last flush).
+    // step fetched is added to `acc` (StepField, the lane's TraversalStats counts since the last flush).
     // A step pops before it pushes and pushes at most PUSH_MAX entries, so when no lane of
     // the wave is within PUSH_MAX levels of STACK_LDS the whole step stays in LDS.
     static constexpr int PUSH_MAX = 4;
-    uint32_t acc = 0;                   // ST_* fields of the steps since the caller last took them
+    using SF = StepField<LST>;
+    uint32_t acc = 0;                   // SF fields of the steps since the caller last flushed them
     RT_D bool step(const DevScene& sc, const Stack& st) {
         if (__ballot(sp > STACK_LDS - PUSH_MAX || !(cflags & 64u)) == 0ull) return step_impl<true, true>(sc, st);
         return step_impl<false, false>(sc, st);
@@ -754,7 +767,7 @@ struct Traversal {
         if (mode == TM_LEAF) {
             const uint32_t pi = __float_as_uint(F[3].x);
             ++leaf_cur; leaf_list >>= 6;
-            if (pi == ignored) { acc += ST_TOP; return true; }
+            if (pi == ignored) { if (!LST) acc += SF::TOP; return true; }
             const uint32_t type = __float_as_uint(F[3].y) & 0xFFu;
             M34 inv;
             inv.e[0][0] = F[0].x; inv.e[0][1] = F[0].y; inv.e[0][2] = F[0].z; inv.e[0][3] = F[0].w;
@@ -771,7 +784,7 @@ struct Traversal {
                 float tn;
                 if (bv_static(ir, rp, rr, tn)) push<SH>(st, __float_as_uint(F[4].x), tn);
                 mode = TM_MESH;
-                acc += ST_ENTRY;
+                acc += SF::ENTRY;
                 return true;
             }
             if (!LST) {
@@ -779,15 +792,15 @@ struct Traversal {
                 if (type == RT_PRIMITIVE_SPHERE) hit = ray_sphere(ir, F[3].z, t);
                 else if (type == RT_PRIMITIVE_BOX) hit = ray_box(ir, {F[3].z, F[3].w, F[4].x}, t);
                 if (hit) {
-                    if (OCC) { occluded = true; mode = TM_DONE; acc += ST_TOP; return false; }
+                    if (OCC) { occluded = true; mode = TM_DONE; if (!LST) acc += SF::TOP; return false; }
                     code = pi;
                 }
             }
-            acc += ST_TOP;
+            if (!LST) acc += SF::TOP;
             return true;
         }
         if (cur_cnt) {                                             // mesh leaf: triangles in order
-            acc += fresh ? (ST_LEAF | ST_TRIS) : ST_TRIS;
+            acc += fresh ? (SF::LEAF | SF::TRIS) : SF::TRIS;
             Ray r; r.o = co; r.d = cd;
             const uint32_t g0 = tri_off + cur_lf;
 #pragma unroll
@@ -804,9 +817,9 @@ struct Traversal {
             return true;
         }
         has_cur = false;
-        if (LST || mode == TM_MESH) { push_children4<SH, FIN>(st, F); acc += ST_NODE; return true; }
+        if (LST || mode == TM_MESH) { push_children4<SH, FIN>(st, F); acc += SF::NODE; return true; }
         push_children<SH, FIN>(st, F);
-        acc += ST_TOP;
+        if (!LST) acc += SF::TOP;
         return true;
     }
 
@@ -1678,8 +1691,8 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     bool exhausted = false, active = false;
     uint32_t item = 0;
     Traversal<OCC, LST> tr;
-    StepCounts<LST> tally;
-    static_assert(STEPS_PER_REFILL < 16, "StepCounts' 4-bit fields");
+    StepCounts<LST> tally;                              // checked after every refill round
+    static_assert(STEPS_PER_REFILL <= StepField<LST>::MARGIN, "StepCounts: a round's steps fit a field's upper half");
     auto finish = [&]() {
         if (OCC) {
             if (!tr.occluded) {
@@ -1742,9 +1755,9 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                 if (!tr.step(sc, st)) { finish(); active = false; break; }
             }
         }
-        tally.acc = tr.acc; tr.acc = 0;
-        tally.flush();                                  // every lane is here
+        tally.check(tr.acc);                            // every lane is here
     }
+    tally.flush(tr.acc);
     tally.commit(cnt->trav[blockIdx.x % NSHARD], OCC ? 1 : 0);
 }
 
@@ -2265,10 +2278,9 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
             }
             for (int k = 1; __ballot(tracing); ++k) {
                 if (tracing && !tr.step(sc, stk)) tracing = false;
-                if (k % STEPS_PER_REFILL == 0) { tally[0].acc = tr.acc; tr.acc = 0; tally[0].flush(); }
+                tally[0].check(tr.acc);
             }
-            tally[0].acc = tr.acc;
-            tally[0].flush();
+            tally[0].flush(tr.acc);
             if (active && pro.bvh && tr.code != RT_HIT_MISS) h = tr.result();
         }
         // one bounce
@@ -2297,10 +2309,9 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
             }
             for (int k = 1; __ballot(tracing); ++k) {
                 if (tracing && !tr.step(sc, stk)) tracing = false;
-                if (k % STEPS_PER_REFILL == 0) { tally[1].acc = tr.acc; tr.acc = 0; tally[1].flush(); }
+                tally[1].check(tr.acc);
             }
-            tally[1].acc = tr.acc;
-            tally[1].flush();
+            tally[1].flush(tr.acc);
             if (cast_shadow && !spro.occluded && (!spro.bvh || !tr.occluded)) total = add(total, sh_c);
         }
         n_shadow += cast_shadow ? 1u : 0u;
