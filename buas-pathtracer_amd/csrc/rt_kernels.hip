@@ -556,7 +556,9 @@ extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // A wave's step counts.  flush(acc), at a point every lane of the wave reaches, sums the lanes'
 // Traversal::acc (StepField) over the wave with DPP reductions, two fields per reduction (64 x 255
 // fits 16 bits), into the wave's totals, which stay in SGPRs, and clears it; check(acc) flushes
-// once some lane has a field at half its range; commit: one lane adds the totals to the counters.
+// once some lane has a field at half its range (k_trace, after each refill round: a ballot); k_drain,
+// whose walks take one step per lane per iteration, flushes every H iterations instead (8 fewer
+// VGPRs there than the ballot); commit: one lane adds the totals to the counters.
 template <bool LST>
 struct StepCounts {
     using F = StepField<LST>;
@@ -2278,7 +2280,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
             }
             for (int k = 1; __ballot(tracing); ++k) {
                 if (tracing && !tr.step(sc, stk)) tracing = false;
-                tally[0].check(tr.acc);
+                if (k % StepField<LST>::H == 0) tally[0].flush(tr.acc);   // one step per lane per k
             }
             tally[0].flush(tr.acc);
             if (active && pro.bvh && tr.code != RT_HIT_MISS) h = tr.result();
@@ -2309,7 +2311,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
             }
             for (int k = 1; __ballot(tracing); ++k) {
                 if (tracing && !tr.step(sc, stk)) tracing = false;
-                tally[1].check(tr.acc);
+                if (k % StepField<LST>::H == 0) tally[1].flush(tr.acc);   // one step per lane per k
             }
             tally[1].flush(tr.acc);
             if (cast_shadow && !spro.occluded && (!spro.bvh || !tr.occluded)) total = add(total, sh_c);
