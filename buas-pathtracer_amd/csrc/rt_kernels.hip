@@ -2709,7 +2709,15 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         }
         if (t == 0) {
             skip = sk;
-            if (sk) cnt->res_from = cnt->res_to = 0;        // its last passes are resolved already
+            if (sk) {
+                // done: the passes the bookkeep that found it complete could not plan (an iteration
+                // without a resolve after it) are resolved after this one, on the device, instead of
+                // waiting for the host's BK_FINAL
+                const bool last = plan.mode && rcur < plan.pass1;
+                cnt->res_from = last ? rcur : 0u;
+                cnt->res_to = last ? plan.pass1 : 0u;
+                if (last) cnt->res_cursor = plan.pass1;
+            }
             if (it_phase && !sk) {
                 const unsigned long long lm = lim < total ? lim : total;
                 const unsigned long long rem = lm > next ? lm - next : 0ull;      // remaining_samples()
