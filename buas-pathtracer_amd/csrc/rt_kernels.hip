@@ -3408,6 +3408,16 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         b(RT_KERNEL_GENERATE);
         k_generate<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE);
+        if (fuse) {
+            k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
+            if (s->ds.listed_only) {
+                if (env) k_drain<true, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<true, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+            } else {
+                if (env) k_drain<false, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<false, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+            }
+        }
         b(RT_KERNEL_EXTEND);
         if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
@@ -3424,19 +3434,6 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         e(RT_KERNEL_CONNECT);
-        // the fused drain after them: in the iteration it runs in, extend / shade / connect exit at
-        // once, so they go first and the drain is followed at once by the bookkeep and the resolve of
-        // the partition's last passes (their launches no longer wait for room behind the drain)
-        if (fuse) {
-            k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
-            if (s->ds.listed_only) {
-                if (env) k_drain<true, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-                else k_drain<true, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-            } else {
-                if (env) k_drain<false, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-                else k_drain<false, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-            }
-        }
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
         const bool res = stream_splat && (plan || r.drain);
