@@ -520,9 +520,24 @@ static inline int ray_intersect_triangle(const Ray* ray, V3 a, V3 b, V3 c,
    (:378-380) -- not when an occlusion query returns from inside it (:297-299). */
 enum { TS_CALLS, TS_BVH, TS_NODES, TS_LEAVES, TS_N };
 
+/* The GPU's degenerate-axis pruning (bv_static in buas-pathtracer_amd/csrc/rt_kernels.hip, mesh BVHs
+   only): for a ray with a direction component exactly 0, a node whose slab on that axis excludes the
+   ray's coordinate by more than 1 % of the node's largest half extent plus 1e-5 of its position is
+   skipped (it holds no triangle the ray can hit; the reference's NaN slab keeps it).  The results are
+   the reference's either way; only the GPU walk's node and leaf counts see it. */
+static inline int gpu_pruned(const Ray* ray, V3 p, V3 r) {
+    const int zx = ray->d.x == 0.0f, zy = ray->d.y == 0.0f, zz = ray->d.z == 0.0f;
+    if (!(zx || zy || zz)) return 0;
+    const V3 rel = sub(ray->o, p);
+    const float margin = 0.01f*mx(r.x, mx(r.y, r.z)) + 1e-5f*mx(fabsf(p.x), mx(fabsf(p.y), fabsf(p.z)));
+    return (zx && fabsf(rel.x) > r.x + margin) || (zy && fabsf(rel.y) > r.y + margin) ||
+           (zz && fabsf(rel.z) > r.z + margin);
+}
+
 /* intersect_mesh, BVHStorage_Scalar path (RT/intersection.cpp:243-401).  ts: the reference's
    TraversalStats of the query kind (or NULL); leaves_all: leaves entered, counted whether or not
-   the traversal returns early (the GPU walk's count, gpu_walk_query below; or NULL). */
+   the traversal returns early (the GPU walk's count, gpu_walk_query below; or NULL), in which case
+   the walk also applies the GPU's degenerate-axis pruning (gpu_pruned). */
 static int intersect_mesh(const rt_mesh* mesh, const Ray* ray, int occlusion, float* out_t,
                           uint32_t* out_tri, V3* out_uvw, V3* out_a, V3* out_b, V3* out_c,
                           uint64_t* ts, uint64_t* leaves_all) {
@@ -535,7 +550,8 @@ static int intersect_mesh(const rt_mesh* mesh, const Ray* ray, int occlusion, fl
     while (at > 0) {
         const rt_bvh_node* node = &mesh->nodes[stack[--at]];
         ++trav;
-        if (ray_intersect_bv(ray, node->bv_p, node->bv_r, *out_t)) {
+        if (ray_intersect_bv(ray, node->bv_p, node->bv_r, *out_t) &&
+            !(leaves_all && gpu_pruned(ray, node->bv_p, node->bv_r))) {
             if (node->count) {
                 ++leaves;
                 uint32_t first = node->left_first;
@@ -690,12 +706,10 @@ static int intersect_scene_internal(const rt_scene_desc* scene, const Ray* ray, 
        prologue, walks the whole top level from the root in the reference's front-to-back order,
        starting at the prologue's t, entering every mesh instance whose leaf passes (for the scene
        whose top level is too large, these entries are the GPU's mesh_intersection_count).
-   The leaves are the BVH4's (the BVH2's leaves), walked here in the BVH2's front-to-back order:
-   the GPU's BVH4 child order finds some hits sooner and culls leaves this walk still enters, and
-   its pruning of nodes that a ray with an exactly-zero direction component cannot hit (bv_static)
-   is not restated either, so the GPU's leaf counts are close to these (closest-hit queries 2.6e-4
-   to 4.5e-4 below on C3, C4 and a C5 shard; shadow queries 2.7e-3 below on C3, within 1.3e-5 on
-   C4 and C5), not equal to them.  GW_CALLS is exact. */
+   The leaves are the BVH4's (the BVH2's leaves, which it visits in the BVH2's depth-first order),
+   walked here in the BVH2's front-to-back order with the GPU's pruning of nodes that a ray with an
+   exactly-zero direction component cannot hit (gpu_pruned), so the GPU's leaf counts equal these
+   up to float ties (a few leaves in 10^7 on C3 and C4 at 480x270).  GW_CALLS is exact. */
 enum { GW_CALLS, GW_ENTRIES, GW_LEAVES, GW_N };
 static int g_gw_on = 0;
 static uint32_t g_gw_mlist = 4;
@@ -762,7 +776,7 @@ static int gw_top(const rt_scene_desc* sc, const Ray* ray, const int neg[3], int
                     if (list || calls) g[GW_CALLS]++;
                     if (list) {
                         const rt_bvh_node* root = &sc->meshes[prim->mesh_index].nodes[0];
-                        if (ray_intersect_bv(&ir, root->bv_p, root->bv_r, *t)) {
+                        if (ray_intersect_bv(&ir, root->bv_p, root->bv_r, *t) && !gpu_pruned(&ir, root->bv_p, root->bv_r)) {
                             if (*n < 64) list[*n] = pi;
                             ++*n;
                         }

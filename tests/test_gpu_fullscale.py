@@ -95,9 +95,11 @@ def check_traversal(gs, walk):
         t = gs.traversal[k]
         # the instances the walk reaches: exact, query kind by query kind
         assert t.mesh_intersection_count == walk["calls"][k], (k, t.mesh_intersection_count, walk["calls"][k])
-        # leaves entered: not restated exactly.  Measured GPU - restated: closest
-        # C3 -4.0e-4, C4 -2.6e-4, C5 shard -4.5e-4; shadow C3 -2.7e-3, C4 -1.3e-5, C5 shard +2e-7
-        assert abs(t.mesh_leaf_traversals - walk["leaves"][k]) <= 5e-3 * walk["leaves"][k], \
+        # leaves entered: the restatement walks the BVH2 with the GPU's degenerate-axis pruning; the BVH4
+        # skips a level's box test, and where float rounding lets a child pass a test its parent fails
+        # (or a tie at tn == t) the GPU enters a leaf more.  Measured GPU - restated: +1 to +188 leaves,
+        # at most 3.0e-7, on C3, C4 and the C5 shard
+        assert abs(t.mesh_leaf_traversals - walk["leaves"][k]) <= 1e-6 * walk["leaves"][k], \
             (k, t.mesh_leaf_traversals, walk["leaves"][k])
         # a BVH4 step is an instance's entry, an interior node or up to two triangles of a leaf
         assert t.mesh_bvh_traversals >= t.mesh_node_traversals + t.mesh_leaf_traversals

@@ -347,7 +347,10 @@ def test_top_level_paths(rt, env, monkeypatch):
     assert gstats.closest_hit_rays == cstats.closest_hit_rays or same < 1.0
     assert calls == walk.result["calls"]
     for k in range(2):
-        assert walk.result["leaves"][k] * (1 - 1e-3) <= leaves[k] <= walk.result["leaves"][k]
+        # leaves entered: the restated walk applies the GPU's degenerate-axis pruning; the BVH4's skipped
+        # level can let a few more through (test_gpu_fullscale.py: at most 3e-7 of them)
+        assert abs(leaves[k] - walk.result["leaves"][k]) <= max(2, 1e-5 * walk.result["leaves"][k]), \
+            (k, leaves[k], walk.result["leaves"][k])
 
 
 @pytest.mark.parametrize("how", ["budget", "mode"])
