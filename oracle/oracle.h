@@ -93,10 +93,11 @@ void     oracle_set_env_sampling(int mode);
  * (rt_abi.h).  oracle_gpu_walk_stats(1, ...) additionally restates that walk in every query of the
  * following renders (the prologue's order, mlist_max = RT_MLIST_MAX of the GPU run, top_prologue = 0
  * as RT_TOP_PROLOGUE=0) and resets the sums; oracle_gpu_walk_result gives them per kind (closest-hit,
- * then shadow): mesh instances reached (the GPU's mesh_intersection_count), mesh instances entered by
- * the trace kernels, leaves entered (the GPU's mesh_leaf_traversals). */
+ * then shadow), five each: mesh instances reached (the GPU's mesh_intersection_count), mesh instances
+ * entered by the trace kernels, leaves entered (mesh_leaf_traversals), BVH4 interior nodes expanded
+ * (mesh_node_traversals), triangle steps (mesh_bvh_traversals = entered + nodes + triangle steps). */
 void     oracle_gpu_walk_stats(int on, uint32_t mlist_max, int top_prologue);
-void     oracle_gpu_walk_result(uint64_t out[6]);
+void     oracle_gpu_walk_result(uint64_t out[10]);
 /* Mitchell–Netravali and friends (RT/reconstruction_filters.cpp:8-95) + LUT */
 int      oracle_load_filter(const char* name, rt_filter_cache* out);
 

@@ -141,8 +141,9 @@ class env_sampling:
 class gpu_walk:
     """with gpu_walk() as g: the oracle's renders also restate the GPU library's own traversal walk
     (oracle_gpu_walk_stats); afterwards g.result = {"calls": [closest, shadow], "entries": [...],
-    "leaves": [...]}: the GPU's rt_stats::traversal mesh_intersection_count, the mesh instances its
-    trace kernels enter, and its mesh_leaf_traversals for the same queries."""
+    "leaves": [...], "nodes": [...], "bvh": [...]}: the GPU's rt_stats::traversal
+    mesh_intersection_count, the mesh instances its trace kernels enter, its mesh_leaf_traversals,
+    mesh_node_traversals (BVH4 nodes) and mesh_bvh_traversals (entries + nodes + triangle steps)."""
 
     def __init__(self, mlist_max=4, top_prologue=True):
         self.mlist_max, self.top = mlist_max, top_prologue
@@ -153,9 +154,10 @@ class gpu_walk:
         return self
 
     def __exit__(self, *exc):
-        out = (C.c_uint64 * 6)()
+        out = (C.c_uint64 * 10)()
         load().oracle_gpu_walk_result(out)
         load().oracle_gpu_walk_stats(0, 4, 1)
-        self.result = {"calls": [int(out[0]), int(out[3])], "entries": [int(out[1]), int(out[4])],
-                       "leaves": [int(out[2]), int(out[5])]}
+        g = lambda i: [int(out[i]), int(out[5 + i])]
+        self.result = {"calls": g(0), "entries": g(1), "leaves": g(2), "nodes": g(3),
+                       "bvh": [g(1)[k] + g(3)[k] + g(4)[k] for k in range(2)]}
         return False

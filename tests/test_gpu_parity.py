@@ -351,6 +351,9 @@ def test_top_level_paths(rt, env, monkeypatch):
         # level can let a few more through (test_gpu_fullscale.py: at most 3e-7 of them)
         assert abs(leaves[k] - walk.result["leaves"][k]) <= max(2, 1e-5 * walk.result["leaves"][k]), \
             (k, leaves[k], walk.result["leaves"][k])
+        for f, key in (("mesh_node_traversals", "nodes"), ("mesh_bvh_traversals", "bvh")):
+            g, r = int(getattr(gstats.traversal[k], f)), walk.result[key][k]
+            assert abs(g - r) <= max(4, 1e-5 * r), (k, f, g, r)
 
 
 @pytest.mark.parametrize("how", ["budget", "mode"])
