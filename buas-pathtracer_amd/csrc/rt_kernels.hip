@@ -1663,8 +1663,9 @@ constexpr int TB = 256;                     // threads per persistent trace bloc
 constexpr uint32_t CHUNK = 256;             // queue items a wave takes per fetch
 constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 
-// 4 waves per SIMD (128 VGPRs): the BVH4 step wants ~138, i.e. 3 waves; the few
-// spilled values cost less than the lost occupancy (C3: 5446 vs 5389 Mrays/s)
+// 4 waves per SIMD: the listed builds fit in 112 / 107 VGPRs without spills, and the
+// block's 16-entry LDS stack (32.8 KB) allows 4 blocks per CU anyway.  5 waves need a
+// 12-entry stack and 96 VGPRs (spills): -10 % C3 (profiles/r04_lds_stack_ab.txt)
 #define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
