@@ -1,0 +1,129 @@
+"""Edge cases of the render path through the GPU against the oracle: degenerate scenes (sky only,
+planes only, no meshes, a one-triangle mesh), ragged and tiny frames, and the settings' limits
+(one sample per pixel, the deepest path the ABI accepts, and the first one it rejects).
+
+Each case is checked as tests/test_gpu_scenes.py checks a scene (`_compare`): per-sample radiance
+bit-exact on a random sample list (>= 99.9 %), the exact-splat frame against the oracle's
+single-thread frame (the reference's splat order, RT/raytracer.cpp:187-259) bit for bit on
+>= 99.9 % of pixels and rel L2 <= 1e-6, the streaming splat within rel L2 <= 1e-5, equal ray counts.
+"""
+import numpy as np
+import pytest
+
+import oracle_binding as ob
+from test_gpu_scenes import _compare
+
+
+KINDS = ["sky", "planes", "sphere_light", "one_triangle", "flat_triangle"]
+
+
+def _camera(rt, w, h, p=(0.0, 1.0, -5.0), at=(0.0, 1.0, 0.0)):
+    cam = rt.abi.Camera()
+    cam.vfov = rt.DEG_TO_RAD * 50.0
+    cam.aspect_ratio = w / h
+    cam.lens_radius = 0.0
+    cam.focus_distance = 10.0
+    cam.p = rt.v3(*p)
+    rt.aim_camera_at(cam, at)
+    rt.recompute_camera(cam)
+    return cam
+
+
+def degenerate_scene(rt, kind):
+    """A scene that exercises one empty or minimal part of the scene model (RT/scene.h): no
+    primitive at all (only the reference's null primitive 0), planes without a BVH, analytic
+    primitives without a mesh, a mesh of one triangle (a one-leaf mesh BVH), and the same triangle
+    lying in z = 0, whose zero-thickness box no ray enters: the reference's slab test needs
+    tn < tf strictly (RT/intersection.cpp:128), so the triangle is invisible there and here."""
+    s = rt.Scene()
+    m = s.add_diffuse_material((0.6, 0.5, 0.4), 1.5)
+    light = s.add_emissive_material((8.0, 7.0, 6.0))
+    if kind in ("planes", "sphere_light"):
+        s.add_plane(m, (0.0, 1.0, 0.0), -1.0)
+    if kind == "sphere_light":
+        s.add_sphere(m, 1.0, rt.translate((0.0, 1.0, 0.0)))
+    if kind in ("sphere_light", "one_triangle", "flat_triangle"):
+        s.add_sphere(light, 0.5, rt.translate((0.0, 3.0, -3.0)))   # above the camera's view
+    if kind in ("one_triangle", "flat_triangle"):
+        dz = 0.5 if kind == "one_triangle" else 0.0
+        tris = np.array([[[-1.0, 0.0, dz], [0.0, 2.0, 0.0], [1.0, 0.0, -dz]]], np.float32)   # normal towards -z
+        s.add_mesh(m, s.create_mesh(tris), rt.identity())
+    s.set_sky((0.6, 0.7, 0.9), (0.1, 0.1, 0.1))
+    s.create_scene_bvh()
+    return s
+
+
+def test_degenerate_scenes_render_on_the_oracle(rt):
+    """CPU: the oracle renders every degenerate scene deterministically, and the scenes differ
+    where they should: a frame with no diffuse surface in view sends no shadow ray (sky only, the
+    flat triangle), the tilted triangle is seen."""
+    w, h = 16, 12
+    cam = _camera(rt, w, h)
+    st, _ = rt.default_settings()
+    st.samples_per_pixel = 2
+    fc = rt.load_reconstruction_kernel("Mitchell Netravali")
+    frames = {}
+    for kind in KINDS:
+        scene = degenerate_scene(rt, kind)          # desc() points into the live host scene
+        d = scene.desc()
+        a, sa = ob.render(d, cam, st, fc, w, h, rng_mode=0, threads=2)
+        b, sb = ob.render(d, cam, st, fc, w, h, rng_mode=0, threads=2)
+        assert np.array_equal(a, b) and sa.closest_hit_rays == sb.closest_hit_rays
+        frames[kind] = (a, sa)
+    assert frames["sky"][1].shadow_rays == 0 and frames["flat_triangle"][1].shadow_rays == 0
+    assert frames["one_triangle"][1].shadow_rays > 0 and frames["sphere_light"][1].shadow_rays > 0
+    assert not np.array_equal(frames["flat_triangle"][0], frames["one_triangle"][0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", KINDS)
+def test_degenerate_scene_gpu_matches_oracle(rt, kind):
+    w, h = 48, 36
+    cam = _camera(rt, w, h)
+    st, _ = rt.default_settings()
+    st.samples_per_pixel = 8
+    fc = rt.load_reconstruction_kernel("Mitchell Netravali")
+    _compare(rt, f"degenerate_{kind}", degenerate_scene(rt, kind), cam, st, fc, w, h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("w,h", [(1, 1), (5, 3), (65, 33), (130, 7)])
+def test_ragged_frames_gpu_match_oracle(rt, w, h):
+    """Frames smaller than one 64x64 tile, one pixel past a tile in each direction, and a
+    strip: the tile grid, the pixel map and the resolve's edges (RT/raytracer.cpp:366-372)."""
+    scene, cam, st, fc, post = rt.load_preset("c1", w, h)
+    st.samples_per_pixel = 4
+    _compare(rt, f"ragged_{w}x{h}", scene, cam, st, fc, w, h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spp,bounces", [(1, 4), (4, 63)])
+def test_settings_limits_gpu_match_oracle(rt, spp, bounces):
+    """One sample per pixel, and the deepest path the material stack allows (max_bounce_count
+    63): in the closed Cornell box without Russian roulette a sample traces ~54 closest-hit rays,
+    most paths run all 63 bounces."""
+    w, h = 64, 48
+    scene, cam, st, fc, post = rt.load_preset("cornell_box", w, h)
+    st.samples_per_pixel = spp
+    st.max_bounce_count = bounces
+    st.russian_roulette = 0
+    _compare(rt, f"limits_spp{spp}_depth{bounces}", scene, cam, st, fc, w, h)
+
+
+@pytest.mark.gpu
+def test_max_bounce_count_over_limit_rejected(rt):
+    """max_bounce_count 64 is past the 64-entry material stack's levels: RT_ERROR_INVALID, no
+    frame (DESIGN.md §2 Errors)."""
+    w, h = 16, 16
+    scene, cam, st, fc, post = rt.load_preset("c1", w, h)
+    st.max_bounce_count = 64
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        with pytest.raises(rt.RenderError) as e:
+            dev.render(cam, st, fc, w, h)
+        assert e.value.code == rt.abi.RT_ERROR_INVALID
+        st.max_bounce_count = 63
+        frame, stats = dev.render(cam, st, fc, w, h)
+        assert stats.samples == w * h * st.samples_per_pixel
+    finally:
+        dev.close()
