@@ -207,7 +207,11 @@ class Scene:
         return {k: getattr(info, k) for k, _ in BvhInfo._fields_}
 
     def desc(self):
-        return lib().rth_scene_desc(self._h).contents
+        """The flattened scene (rt_scene_desc).  Its arrays point into this host scene, so the
+        returned struct keeps the Scene alive (`Scene(...).desc()` on a temporary is safe)."""
+        d = lib().rth_scene_desc(self._h).contents
+        d._scene = self
+        return d
 
 
 def load_preset(name, w, h, asset_dir=None):

@@ -127,3 +127,18 @@ def test_max_bounce_count_over_limit_rejected(rt):
         assert stats.samples == w * h * st.samples_per_pixel
     finally:
         dev.close()
+
+
+def test_desc_keeps_its_scene_alive(rt):
+    """CPU: rt_scene_desc's arrays point into the host scene; the struct the Python host returns
+    holds the Scene, so a desc taken from a temporary stays valid (it once read freed memory)."""
+    import gc
+    d = degenerate_scene(rt, "planes").desc()
+    gc.collect()
+    assert d.plane_count == 1 and d.planes[0].transform_index < d.transform_count
+    cam = _camera(rt, 8, 6)
+    st, _ = rt.default_settings()
+    st.samples_per_pixel = 1
+    fc = rt.load_reconstruction_kernel("Box")
+    frame, stats = ob.render(d, cam, st, fc, 8, 6, rng_mode=0, threads=1)
+    assert stats.samples == 48 and np.isfinite(frame).all()
