@@ -373,6 +373,8 @@ struct Hit {
 struct Stack {
     uint2* lds;         // [STACK_LDS][block] for this block
     uint2* spill;       // [STACK_DEPTH - STACK_LDS][nthreads] global
+    float2* bary;       // [block] the lane's closest-hit barycentrics (v, w), in LDS: out of the
+                        // registers the traversal step holds (the listed extend kernel: 100 -> 96 VGPRs)
     uint32_t lane, block, gtid, nthreads;
     // LDS_ONLY: the caller knows every level it touches is below STACK_LDS
     template <bool LDS_ONLY = false>
@@ -589,7 +591,6 @@ struct Traversal {
                         // | bit 6: finite slabs (finite_box_ray and DevScene::finite_boxes)
     float t;
     uint32_t code, tri;
-    float hv, hw;
     uint32_t ignored;
     int sp, mode, mesh_base;
     uint32_t leaf_cur, leaf_end;        // TM_LEAF: range of bvh_indices slots still to test
@@ -637,7 +638,7 @@ struct Traversal {
         wo = o; wd = d;
         finite_world = false;                                      // debug path: reference max/min chains
         set_world();
-        t = max_t; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
+        t = max_t; code = RT_HIT_MISS; tri = 0; st.bary[st.lane] = make_float2(0.0f, 0.0f);
         ignored = ign; sp = 0; mode = TM_TOP; occluded = false; has_cur = false; listed = false;
         Ray wr = make_ray(o, d, max_t);
         wr.zero = 0u;                                              // no pruning on the world ray
@@ -664,14 +665,15 @@ struct Traversal {
         wo = o; wd = d; co = o; cd = d; cinv = inv_d;
         finite_world = sc.finite_boxes && finite_box_ray(o, inv_d);
         cflags = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u) | (finite_world ? 64u : 0u);
-        t = t0; code = RT_HIT_MISS; tri = 0; hv = 0.0f; hw = 0.0f;
+        t = t0; code = RT_HIT_MISS; tri = 0; st.bary[st.lane] = make_float2(0.0f, 0.0f);
         ignored = ign; sp = 0; occluded = false; has_cur = false;
         if (mlist == MLIST_FULL) {
             mode = TM_TOP; listed = false;
             st.put(sp++, sc.bvh_root_rec, __uint_as_float(0xFF800000u));
         } else {
             mode = TM_LEAF; listed = true;
-            leaf_list = mlist & 0xFFFFFFu; leaf_cur = 0; leaf_end = mlist >> 24;
+            if (LST) leaf_list = mlist;                            // LST: the count stays in bits 24-31
+            else { leaf_list = mlist & 0xFFFFFFu; leaf_cur = 0; leaf_end = mlist >> 24; }
         }
     }
 
@@ -733,12 +735,14 @@ struct Traversal {
     RT_D bool step_impl(const DevScene& sc, const Stack& st) {
         // 1. state changes that need no global memory
         const bool take = mode == TM_MESH && !has_cur;
-        if (take && !pop<SH>(st, sc.mnodes_src + node_off, mesh_base)) {
+        if (take && !pop<SH>(st, sc.mnodes_src + node_off, LST ? 0 : mesh_base)) {
             mode = TM_LEAF;                                        // instance finished
-            set_world();
+            // LST: the next step is the end or a listed instance's leaf step, which sets the
+            // object-space ray from wo / wd itself (nothing reads the world ray in between)
+            if (!LST) set_world();
         }
         const bool fresh = take && mode == TM_MESH;               // a mesh node popped in this step
-        if (mode == TM_LEAF && leaf_cur == leaf_end) {
+        if (mode == TM_LEAF && (LST ? (leaf_list >> 24) == 0u : leaf_cur == leaf_end)) {
             if (LST) { mode = TM_DONE; return false; }           // the mesh list is the whole walk
             mode = TM_TOP;
         }
@@ -768,7 +772,8 @@ struct Traversal {
         // 3. arithmetic
         if (mode == TM_LEAF) {
             const uint32_t pi = __float_as_uint(F[3].x);
-            ++leaf_cur; leaf_list >>= 6;
+            if (LST) leaf_list = ((leaf_list >> 6) & 0x3FFFFu) | ((leaf_list & 0xFF000000u) - 0x01000000u);
+            else { ++leaf_cur; leaf_list >>= 6; }
             if (pi == ignored) { if (!LST) acc += SF::TOP; return true; }
             const uint32_t type = __float_as_uint(F[3].y) & 0xFFu;
             M34 inv;
@@ -781,7 +786,7 @@ struct Traversal {
                 co = ir.o; cd = ir.d; cinv = ir.inv_d;
                 cflags = ir.neg | (ir.zero << 3) | ((sc.finite_boxes && finite_box_ray(ir.o, ir.inv_d)) ? 64u : 0u);
                 inst = pi; node_off = __float_as_uint(F[3].z); tri_off = __float_as_uint(F[3].w);
-                mesh_base = sp;
+                if (!LST) mesh_base = sp;              // LST: the stack holds this mesh only
                 const V3 rp = {F[4].y, F[4].z, F[4].w}, rr = {F[5].x, F[5].y, F[5].z};
                 float tn;
                 if (bv_static(ir, rp, rr, tn)) push<SH>(st, __float_as_uint(F[4].x), tn);
@@ -805,15 +810,18 @@ struct Traversal {
             acc += fresh ? (SF::LEAF | SF::TRIS) : SF::TRIS;
             Ray r; r.o = co; r.d = cd;
             const uint32_t g0 = tri_off + cur_lf;
+            float bv = 0.0f, bw = 0.0f;
+            bool hit = false;
 #pragma unroll
             for (uint32_t j = 0; j < TRI_FETCH; ++j)
                 if (j < cur_cnt) {
                     float v, w;
                     if (ray_triangle(r, ld3(F[3*j]), ld3(F[3*j + 1]), ld3(F[3*j + 2]), t, v, w)) {
                         if (OCC) { occluded = true; mode = TM_DONE; return false; }
-                        code = inst; tri = g0 + j; hv = v; hw = w;   // t only decreases: closest so far
+                        code = inst; tri = g0 + j; bv = v; bw = w; hit = true;   // t only decreases: closest so far
                     }
                 }
+            if (hit) st.bary[st.lane] = make_float2(bv, bw);
             if (cur_cnt > TRI_FETCH) { cur_lf += TRI_FETCH; cur_cnt -= TRI_FETCH; }
             else has_cur = false;
             return true;
@@ -825,8 +833,9 @@ struct Traversal {
         return true;
     }
 
-    RT_D Hit result() const {
-        Hit h; h.t = t; h.code = OCC ? (occluded ? 0u : RT_HIT_MISS) : code; h.tri = tri; h.v = hv; h.w = hw;
+    RT_D Hit result(const Stack& st) const {
+        const float2 b = st.bary[st.lane];
+        Hit h; h.t = t; h.code = OCC ? (occluded ? 0u : RT_HIT_MISS) : code; h.tri = tri; h.v = b.x; h.w = b.y;
         return h;
     }
 };
@@ -1663,10 +1672,14 @@ constexpr int TB = 256;                     // threads per persistent trace bloc
 constexpr uint32_t CHUNK = 256;             // queue items a wave takes per fetch
 constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 
-// 4 waves per SIMD: the listed builds fit in 112 / 107 VGPRs without spills, and the
-// block's 16-entry LDS stack (32.8 KB) allows 4 blocks per CU anyway.  5 waves need a
-// 12-entry stack and 96 VGPRs (spills): -10 % C3 (profiles/r04_lds_stack_ab.txt)
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+// VGPR budget.  The block's LDS (a 16-entry stack + the hit barycentrics, 34.8 KB) allows 4
+// blocks per CU, i.e. 4 trace waves per SIMD, whatever the registers.  The LDS is dynamic so
+// that the compiler does not see that cap and keeps the listed builds in a 5-wave budget:
+// 96 / 86 VGPRs without spills, which leaves room for two 64-VGPR k_shade waves beside four
+// trace waves instead of one (the 112-VGPR build).  The top-level builds keep the 4-wave
+// budget (118 / 114 VGPRs; at 96 they spill).
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LST ? 5 : 4)))
+constexpr size_t TRACE_LDS = sizeof(uint2)*STACK_LDS*TB + sizeof(float2)*TB;   // dynamic, per block
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
@@ -1678,9 +1691,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
     // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
     __builtin_amdgcn_s_setprio(1);
-    __shared__ uint2 lds_stack[STACK_LDS*TB];
+    extern __shared__ uint2 trace_lds[];                 // TRACE_LDS bytes: the stack, then the barycentrics
     Stack st;
-    st.lds = lds_stack; st.spill = spill; st.lane = threadIdx.x; st.block = TB;
+    st.lds = trace_lds; st.spill = spill; st.bary = reinterpret_cast<float2*>(trace_lds + STACK_LDS*TB);
+    st.lane = threadIdx.x; st.block = TB;
     st.gtid = blockIdx.x*TB + threadIdx.x; st.nthreads = gridDim.x*TB;
     __shared__ uint32_t qlen[NSHARD];
     if (threadIdx.x < NSHARD) qlen[threadIdx.x] = OCC ? cnt->shadow_count[threadIdx.x][0] : cnt->ext_count[cur][threadIdx.x][0];
@@ -1689,7 +1703,6 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     // skips exhausted shards without an atomic)
     uint32_t shard = blockIdx.x % NSHARD, tried = 0;
     const uint32_t lane = __lane_id();
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
     uint32_t chunk_next = 0, chunk_end = 0;
     bool exhausted = false, active = false;
     uint32_t item = 0;
@@ -1708,7 +1721,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             }
         } else if (tr.code != RT_HIT_MISS) {                  // a BVH hit; else k_shade's plane result stands
             const uint32_t slot = item;                       // the path's slot (from the record)
-            const Hit h = tr.result();
+            const Hit h = tr.result(st);
             stnt(&pool.hit[slot], make_float4(h.t, __uint_as_float(h.code), __uint_as_float(h.tri), h.v));
             stnt(&pool.hit_w[slot], h.w);
         }
@@ -1726,7 +1739,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                     if (lane == (uint32_t)leader &&
                         __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < len)
                         base = atomicAdd(head, CHUNK);
-                    base = __shfl(base, leader);
+                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);   // wave-uniform: SGPRs
                     if (base < len) {
                         chunk_next = shard*pool.shard_cap + base;
                         chunk_end = shard*pool.shard_cap + min(base + CHUNK, len);
@@ -1739,7 +1752,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                 if (!got) { exhausted = true; break; }
             }
             const uint32_t avail = chunk_end - chunk_next;
-            const uint32_t rank = (uint32_t)__popcll(idle & lt_mask);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (!active && rank < avail) {
                 item = chunk_next + rank;
                 if (OCC) item = pool.sh_slot[item];               // the k_shade slot that staged the ray
@@ -2193,8 +2206,9 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                                                uint2* spill) {
     if (!cnt->fused || cnt->done) return;                              // uniform
     __shared__ uint2 lds_stack[STACK_LDS*DTB];
+    __shared__ float2 lds_bary[DTB];
     Stack stk;
-    stk.lds = lds_stack; stk.spill = spill; stk.lane = threadIdx.x; stk.block = DTB;
+    stk.lds = lds_stack; stk.spill = spill; stk.bary = lds_bary; stk.lane = threadIdx.x; stk.block = DTB;
     stk.gtid = blockIdx.x*DTB + threadIdx.x; stk.nthreads = gridDim.x*DTB;
     __shared__ uint32_t qlen[NSHARD];
     if (threadIdx.x < NSHARD) qlen[threadIdx.x] = cnt->drain_count[threadIdx.x][0];
@@ -2284,7 +2298,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                 if (k % StepField<LST>::H == 0) tally[0].flush(tr.acc);   // one step per lane per k
             }
             tally[0].flush(tr.acc);
-            if (active && pro.bvh && tr.code != RT_HIT_MISS) h = tr.result();
+            if (active && pro.bvh && tr.code != RT_HIT_MISS) h = tr.result(stk);
         }
         // one bounce
         bool done = false, cast_shadow = false;
@@ -2802,8 +2816,9 @@ template <bool OCC>
 __global__ void __launch_bounds__(128) k_debug_intersect(DevScene sc, const rt_ray_query* rays, rt_hit_record* out,
                                                          uint32_t n, uint2* spill) {
     __shared__ uint2 lds_stack[STACK_LDS*128];
+    __shared__ float2 lds_bary[128];
     Stack st;
-    st.lds = lds_stack; st.spill = spill; st.lane = threadIdx.x; st.block = 128;
+    st.lds = lds_stack; st.spill = spill; st.bary = lds_bary; st.lane = threadIdx.x; st.block = 128;
     st.gtid = blockIdx.x*128 + threadIdx.x; st.nthreads = gridDim.x*128;
     uint32_t i = blockIdx.x*blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -2811,7 +2826,7 @@ __global__ void __launch_bounds__(128) k_debug_intersect(DevScene sc, const rt_r
     Traversal<OCC> tr;
     tr.init(sc, st, rv3(rq.o), rv3(rq.d), rq.max_t, rq.ignored_primitive);
     while (tr.mode != TM_DONE && tr.step(sc, st)) {}
-    const Hit h = tr.result();
+    const Hit h = tr.result(st);
     rt_hit_record r;
     memset(&r, 0, sizeof(r));
     r.t = h.t;
@@ -3420,8 +3435,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             }
         }
         b(RT_KERNEL_EXTEND);
-        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else k_trace<false, false><<<s->trace_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else k_trace<false, false><<<s->trace_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         if (env) {
             if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
@@ -3432,8 +3447,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else k_trace<true, false><<<s->connect_grid, TB, 0, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else k_trace<true, false><<<s->connect_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         e(RT_KERNEL_CONNECT);
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
@@ -4059,7 +4074,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("hipGetDeviceProperties"); return fail(RT_ERROR_DEVICE); }
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, TB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, TB, TRACE_LDS) != hipSuccess || per_cu < 1) per_cu = 1;
         s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
         // Persistent trace blocks: 75 % of one full-occupancy wave of blocks (RT_TRACE_GRID_PCT).
         // Four partitions run their trace launches side by side; a full grid per launch left
