@@ -1531,7 +1531,11 @@ RT_D V2 sample_jitter(const DevScene& sc, const rt_settings& st, const FramePara
 // sampler tables and the ray prologue's tables, which stay in HBM and are read through L2 and the
 // scalar cache: a block needs no LDS copy of the scene, so it skips that copy, its barrier and its
 // LDS footprint.
-__global__ void __launch_bounds__(BLOCK) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
+// SGPR budget: a wave holds ceil(sgpr/16)*16 + 16 of the SIMD's 800 SGPRs.  Left alone the compiler
+// gives k_generate 102 (a 128-SGPR wave, as many as a trace wave); capped at 80 it needs 78 with no
+// spills (96 per wave), so a generate wave finds room beside the trace waves sooner: a rank's share
+// of 8 +1.4 %, C3 / C4 +0.1 / +0.2 % (profiles/r04_sgpr_ab.txt)
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                         Counters* cnt, int cur) {
     // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
     // splat them.  Their NEE contributions from k_connect are in by now.
