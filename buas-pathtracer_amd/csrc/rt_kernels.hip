@@ -2654,11 +2654,13 @@ enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
 // them from the claims; k_generate keeps no counter for them)
 struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0; };
 // Two workgroup sizes, picked per frame by the partition's pool (BK_LARGE_POOL): a pool of 4M paths or
-// more (a whole 1080p frame: 8.4M) takes the 256-thread build (156 VGPRs: 4 waves that find room beside
+// more (a whole 1080p frame: 8.4M) takes the 512-thread build (92 VGPRs: 8 waves that find room beside
 // the other partitions' kernels sooner), a smaller one (a rank's share of a multi-GPU frame: 3.3M) the
 // 1024-thread build (62 VGPRs, 16 waves on one CU).  A/B (profiles/r03b_ab.txt section 14): 256 threads
-// give the full C3 frame +0.5 to +0.9 % and C4 +1.2 to +1.5 %, but rank 0 of 8 -1.9 to -2.8 %.
-constexpr int BK_THREADS_SMALL = 1024, BK_THREADS_LARGE = 256;
+// (156 VGPRs) gave the full C3 frame +0.5 to +0.9 % and C4 +1.2 to +1.5 % over 1024, but rank 0 of 8
+// -1.9 to -2.8 %; with the 96-VGPR trace kernels 512 threads give C3 +1.5 to +2.2 % over 256 and C4 -0.1 to
+// -1.0 % (profiles/r04_bookkeep_ab.txt).
+constexpr int BK_THREADS_SMALL = 1024, BK_THREADS_LARGE = 512;
 constexpr uint32_t BK_LARGE_POOL = 4u << 20;
 template <int BK_THREADS>
 __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
