@@ -370,24 +370,27 @@ struct Hit {
     float v, w;         // barycentrics of that triangle (uvw = (1-v-w, v, w))
 };
 
-struct Stack {
-    uint2* lds;         // [STACK_LDS][block] for this block
-    uint2* spill;       // [STACK_DEPTH - STACK_LDS][nthreads] global
+// SL: the levels kept in LDS (STACK_LDS; the trace kernels' TRACE_STACK_LDS)
+template <int SL>
+struct StackT {
+    uint2* lds;         // [SL][block] for this block
+    uint2* spill;       // [STACK_DEPTH - SL][nthreads] global
     float2* bary;       // [block] the lane's closest-hit barycentrics (v, w), in LDS: out of the
                         // registers the traversal step holds (the listed extend kernel: 100 -> 96 VGPRs)
     uint32_t lane, block, gtid, nthreads;
-    // LDS_ONLY: the caller knows every level it touches is below STACK_LDS
+    // LDS_ONLY: the caller knows every level it touches is below SL
     template <bool LDS_ONLY = false>
     RT_D void put(int level, uint32_t node, float tn) const {
         uint2 e = make_uint2(node, __float_as_uint(tn));
-        if (LDS_ONLY || level < STACK_LDS) lds[level*block + lane] = e;
-        else spill[(size_t)(level - STACK_LDS)*nthreads + gtid] = e;
+        if (LDS_ONLY || level < SL) lds[level*block + lane] = e;
+        else spill[(size_t)(level - SL)*nthreads + gtid] = e;
     }
     template <bool LDS_ONLY = false>
     RT_D uint2 get(int level) const {
-        return (LDS_ONLY || level < STACK_LDS) ? lds[level*block + lane] : spill[(size_t)(level - STACK_LDS)*nthreads + gtid];
+        return (LDS_ONLY || level < SL) ? lds[level*block + lane] : spill[(size_t)(level - SL)*nthreads + gtid];
     }
 };
+using Stack = StackT<STACK_LDS>;
 
 enum { TM_TOP = 0, TM_LEAF = 1, TM_MESH = 2, TM_DONE = 3 };
 
@@ -583,8 +586,9 @@ struct StepCounts {
     }
 };
 
-template <bool OCC, bool LST = false>
+template <bool OCC, bool LST = false, int SL = STACK_LDS>
 struct Traversal {
+    using Stack = StackT<SL>;
     V3 wo, wd;          // world ray
     V3 co, cd, cinv;    // current ray (object space while in a mesh)
     uint32_t cflags;    // current ray: d < 0 per axis (bits 0-2) | d == 0 per axis (bits 3-5, mesh only)
@@ -613,7 +617,7 @@ struct Traversal {
     }
 
     template <bool SH>
-    RT_D void push(const Stack& st, uint32_t rec, float tn) { if (SH || sp < STACK_DEPTH) st.put<SH>(sp++, rec, tn); }
+    RT_D void push(const Stack& st, uint32_t rec, float tn) { if (SH || sp < STACK_DEPTH) st.template put<SH>(sp++, rec, tn); }
 
     // children of an interior node from the fetched sibling pair F[0..3]
     template <bool SH, bool FIN>
@@ -682,7 +686,7 @@ struct Traversal {
     template <bool SH>
     RT_D bool pop(const Stack& st, const rt_bvh_node* nodes, int base) {
         while (sp > base) {
-            const uint2 e = st.get<SH>(--sp);
+            const uint2 e = st.template get<SH>(--sp);
             if (__uint_as_float(e.y) < t) {
                 unpack_node(nodes, e.x, cur_lf, cur_cnt, cur_ax);
                 has_cur = true;
@@ -728,11 +732,26 @@ struct Traversal {
     using SF = StepField<LST>;
     uint32_t acc = 0;                   // SF fields of the steps since the caller last flushed them
     RT_D bool step(const DevScene& sc, const Stack& st) {
-        if (__ballot(sp > STACK_LDS - PUSH_MAX || !(cflags & 64u)) == 0ull) return step_impl<true, true>(sc, st);
+        if (__ballot(sp > SL - PUSH_MAX || !(cflags & 64u)) == 0ull) return step_impl<true, true>(sc, st);
         return step_impl<false, false>(sc, st);
     }
     template <bool SH, bool FIN>
     RT_D bool step_impl(const DevScene& sc, const Stack& st) {
+        bool fresh;
+        const float4* src = step_begin<SH>(sc, st, fresh);
+        if (!src) return false;
+        // unconditional: every array the step reads is padded by FETCH_Q float4 at upload
+        float4 F[FETCH_Q];
+#pragma unroll
+        for (int j = 0; j < FETCH_Q; ++j) F[j] = src[j];
+        return step_end<SH, FIN>(sc, st, F, fresh);
+    }
+    // A step in two halves around its one round of loads (k_trace's cooperative fetch runs the
+    // loads for the whole wave in between).  step_begin: the state changes that need no global
+    // memory; returns the FETCH_Q float4 the step reads, or null once the query is finished
+    // (mode == TM_DONE).  fresh: a mesh node was popped in this step.
+    template <bool SH>
+    RT_D const float4* step_begin(const DevScene& sc, const Stack& st, bool& fresh) {
         // 1. state changes that need no global memory
         const bool take = mode == TM_MESH && !has_cur;
         if (take && !pop<SH>(st, sc.mnodes_src + node_off, LST ? 0 : mesh_base)) {
@@ -741,34 +760,28 @@ struct Traversal {
             // object-space ray from wo / wd itself (nothing reads the world ray in between)
             if (!LST) set_world();
         }
-        const bool fresh = take && mode == TM_MESH;               // a mesh node popped in this step
+        fresh = take && mode == TM_MESH;                          // a mesh node popped in this step
         if (mode == TM_LEAF && (LST ? (leaf_list >> 24) == 0u : leaf_cur == leaf_end)) {
-            if (LST) { mode = TM_DONE; return false; }           // the mesh list is the whole walk
+            if (LST) { mode = TM_DONE; return nullptr; }         // the mesh list is the whole walk
             mode = TM_TOP;
         }
         if (!LST && mode == TM_TOP) {
-            if (!has_cur && !pop<SH>(st, sc.bvh_src, 0)) { mode = TM_DONE; return false; }
+            if (!has_cur && !pop<SH>(st, sc.bvh_src, 0)) { mode = TM_DONE; return nullptr; }
             if (cur_cnt) {                                         // top-level leaf: its primitives in order
                 leaf_cur = cur_lf; leaf_end = cur_lf + cur_cnt; has_cur = false;
                 mode = TM_LEAF;
             }
         }
-        // 2. one round of loads
-        const float4* src;
-        uint32_t nq;
-        if (mode == TM_LEAF) {
-            src = sc.leaf_rec + (size_t)((LST || listed) ? (leaf_list & 63u) : leaf_cur)*LEAF_REC_Q; nq = LEAF_REC_Q;
-        } else if (cur_cnt) {                                      // mesh leaf
-            src = sc.tris + 3*(size_t)(tri_off + cur_lf); nq = 3*min(cur_cnt, TRI_FETCH);
-        } else {                                                   // interior: the sibling pair
-            if (LST || mode == TM_MESH) { src = sc.mnodes4 + 8*(size_t)cur_lf; nq = 8; }
-            else { src = reinterpret_cast<const float4*>((mode == TM_MESH ? sc.mnodes + node_off : sc.bvh) + cur_lf); nq = 4; }
-        }
-        // unconditional: every array the step reads is padded by FETCH_Q float4 at upload
-        (void)nq;
-        float4 F[FETCH_Q];
-#pragma unroll
-        for (int j = 0; j < FETCH_Q; ++j) F[j] = src[j];
+        // 2. what the one round of loads reads
+        if (mode == TM_LEAF)
+            return sc.leaf_rec + (size_t)((LST || listed) ? (leaf_list & 63u) : leaf_cur)*LEAF_REC_Q;
+        if (cur_cnt) return sc.tris + 3*(size_t)(tri_off + cur_lf);                    // mesh leaf
+        if (LST || mode == TM_MESH) return sc.mnodes4 + 8*(size_t)cur_lf;              // mesh BVH4 node
+        return reinterpret_cast<const float4*>(sc.bvh + cur_lf);                       // top level: the sibling pair
+    }
+    // step_end: the arithmetic on what the step fetched (F); returns false once the query is finished
+    template <bool SH, bool FIN>
+    RT_D bool step_end(const DevScene& sc, const Stack& st, const float4 (&F)[FETCH_Q], bool fresh) {
         // 3. arithmetic
         if (mode == TM_LEAF) {
             const uint32_t pi = __float_as_uint(F[3].x);
@@ -1682,8 +1695,62 @@ constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 // 96 / 86 VGPRs without spills, which leaves room for two 64-VGPR k_shade waves beside four
 // trace waves instead of one (the 112-VGPR build).  The top-level builds keep the 4-wave
 // budget (118 / 114 VGPRs; at 96 they spill).
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LST ? 5 : 4)))
-constexpr size_t TRACE_LDS = sizeof(uint2)*STACK_LDS*TB + sizeof(float2)*TB;   // dynamic, per block
+#ifndef RT_TRACE_STACK
+#define RT_TRACE_STACK 16
+#endif
+#ifndef RT_COOP
+#define RT_COOP 0
+#endif
+#ifndef RT_COOP_WAVES
+#define RT_COOP_WAVES 4
+#endif
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_COOP ? RT_COOP_WAVES : LST ? 5 : 4)))
+constexpr int TRACE_STACK_LDS = RT_TRACE_STACK;      // stack levels in LDS (the rest spill to global)
+constexpr bool TRACE_COOP = RT_COOP != 0;            // cooperative step fetch (coop_fetch)
+constexpr size_t COOP_STAGE_Q = 8*(64 + 1);          // float4 per wave: 8 rows of 64 lanes + a 16-byte skew
+constexpr size_t TRACE_LDS = sizeof(uint2)*TRACE_STACK_LDS*TB + sizeof(float2)*TB +
+                             (TRACE_COOP ? sizeof(float4)*COOP_STAGE_Q*(TB/64) : 0);   // dynamic, per block
+
+// The cooperative step fetch: the wave loads its 64 lanes' FETCH_Q float4 (one 128-byte
+// step line each) 8 lanes per line, so each of its 8 wave-instructions touches 8 lines
+// instead of 64 (the per-lane gather moves ~1 lane-line per clock per CU whatever the
+// occupancy; 8 lanes per line straight into LDS moved 1.28-1.43x as many lines at 8-16 waves
+// per CU, tools/microbench_gather.hip).  Every lane of the wave must call it; a lane with
+// src == null fetches nothing (its F is garbage).
+//   Instruction i: lanes 8g..8g+7 load the line of owner L = (g & 1) | i << 1 | (g >> 1) << 4
+//   (its address by ds_bpermute), lane 8g+j its float4 j, with global_load_lds_dwordx4 into
+//   row i of the wave's stage (1 KB, lane-linear: lane l writes slot l).  Row i starts at
+//   i*(1 KB + 16 B).  Owner L reads its float4 m at row (L >> 1) & 7, slot 8g + m: one address
+//   per lane plus immediate offsets.  The 16 lanes of each ds_read_b128 lane group ({0-3,
+//   12-15, 20-27}, ...) hold every row twice with g of both parities, so with the rows' 16-byte
+//   skew they read 16 distinct 16-byte slots of a 256-byte bank row: conflict-free.
+constexpr uint32_t COOP_ROW_Q = 64 + 1;              // float4 per stage row, the skew included
+// A lane with no step (src null) has its loaders read `idle` instead: a valid line, so the
+// loads need no branch (their LDS slots are never read).
+RT_D void coop_fetch(const float4* src, const float4* idle, float4 (&F)[FETCH_Q], float4* stage) {
+    const uint32_t lane = __lane_id();
+    const uint64_t a = (uint64_t)(src ? src : idle);
+    const int alo = (int)(uint32_t)a, ahi = (int)(uint32_t)(a >> 32);
+    const uint32_t g = lane >> 3, j = lane & 7u;
+    const int own4 = (int)(4u*((g & 1u) | ((g >> 1) << 4)));      // 4 x the owner of instruction 0
+    uint32_t lo[8], hi[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {                                  // all 16 in flight together
+        lo[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(own4 + 8*i, alo);
+        hi[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(own4 + 8*i, ahi);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float4* oa = reinterpret_cast<const float4*>((uint64_t)lo[i] | ((uint64_t)hi[i] << 32));
+        __builtin_amdgcn_global_load_lds(oa + j, stage + COOP_ROW_Q*i, 16, 0, 0);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): the DMA has landed in LDS
+    __builtin_amdgcn_wave_barrier();
+    const float4* row = stage + COOP_ROW_Q*((lane >> 1) & 7u) + 8*((lane & 1u) | ((lane >> 4) << 1));
+#pragma unroll
+    for (int m = 0; m < FETCH_Q; ++m) F[m] = row[m];
+    __builtin_amdgcn_wave_barrier();
+}
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
@@ -1695,9 +1762,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
     // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
     __builtin_amdgcn_s_setprio(1);
-    extern __shared__ uint2 trace_lds[];                 // TRACE_LDS bytes: the stack, then the barycentrics
-    Stack st;
-    st.lds = trace_lds; st.spill = spill; st.bary = reinterpret_cast<float2*>(trace_lds + STACK_LDS*TB);
+    extern __shared__ uint2 trace_lds[];   // TRACE_LDS bytes: the stack, the barycentrics, the fetch stages
+    StackT<TRACE_STACK_LDS> st;
+    st.lds = trace_lds; st.spill = spill; st.bary = reinterpret_cast<float2*>(trace_lds + TRACE_STACK_LDS*TB);
+    float4* const stage = reinterpret_cast<float4*>(st.bary + TB) + COOP_STAGE_Q*(threadIdx.x / 64);
     st.lane = threadIdx.x; st.block = TB;
     st.gtid = blockIdx.x*TB + threadIdx.x; st.nthreads = gridDim.x*TB;
     __shared__ uint32_t qlen[NSHARD];
@@ -1710,7 +1778,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     uint32_t chunk_next = 0, chunk_end = 0;
     bool exhausted = false, active = false;
     uint32_t item = 0;
-    Traversal<OCC, LST> tr;
+    Traversal<OCC, LST, TRACE_STACK_LDS> tr;
     StepCounts<LST> tally;                              // checked after every refill round
     static_assert(STEPS_PER_REFILL <= StepField<LST>::MARGIN, "StepCounts: a round's steps fit a field's upper half");
     auto finish = [&]() {
@@ -1770,9 +1838,31 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             idle = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;
-        if (active) {
+        if (!TRACE_COOP) {
+            if (active) {
+                for (int k = 0; k < STEPS_PER_REFILL; ++k) {
+                    if (!tr.step(sc, st)) { finish(); active = false; break; }
+                }
+            }
+        } else {
+            // the wave steps together: the fetch between a step's halves is cooperative
             for (int k = 0; k < STEPS_PER_REFILL; ++k) {
-                if (!tr.step(sc, st)) { finish(); active = false; break; }
+                const unsigned long long act = __ballot(active);
+                if (!act) break;
+                const bool lds_only = __ballot(active && (tr.sp > TRACE_STACK_LDS - tr.PUSH_MAX || !(tr.cflags & 64u))) == 0ull;
+                const float4* src = nullptr;
+                bool fresh = false;
+                if (active) {
+                    src = lds_only ? tr.template step_begin<true>(sc, st, fresh) : tr.template step_begin<false>(sc, st, fresh);
+                    if (!src) { finish(); active = false; }
+                }
+                float4 F[FETCH_Q];
+                coop_fetch(src, sc.tris, F, stage);
+                if (src) {
+                    const bool more = lds_only ? tr.template step_end<true, true>(sc, st, F, fresh)
+                                               : tr.template step_end<false, false>(sc, st, F, fresh);
+                    if (!more) { finish(); active = false; }
+                }
             }
         }
         tally.check(tr.acc);                            // every lane is here
@@ -3150,7 +3240,7 @@ int ensure_partition(rt_scene* s, int k) {
     HIP_OK(hipMalloc(&pt.cnt, sizeof(Counters)));
     HIP_OK(hipHostMalloc(&pt.cnt_host, 3*sizeof(Counters)));
     for (auto& e : pt.chunk_done) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_OK(hipMalloc(&pt.spill, sizeof(uint2)*(size_t)(STACK_DEPTH - STACK_LDS)*s->trace_grid*TB));
+    HIP_OK(hipMalloc(&pt.spill, sizeof(uint2)*(size_t)(STACK_DEPTH - std::min(STACK_LDS, TRACE_STACK_LDS))*s->trace_grid*TB));
     if (k > 0) HIP_OK(hipStreamCreateWithFlags(&pt.own_stream, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&pt.join, hipEventDisableTiming));
     return RT_OK;
