@@ -746,10 +746,11 @@ struct Traversal {
         for (int j = 0; j < FETCH_Q; ++j) F[j] = src[j];
         return step_end<SH, FIN>(sc, st, F, fresh);
     }
-    // A step in two halves around its one round of loads (k_trace's cooperative fetch runs the
-    // loads for the whole wave in between).  step_begin: the state changes that need no global
-    // memory; returns the FETCH_Q float4 the step reads, or null once the query is finished
-    // (mode == TM_DONE).  fresh: a mesh node was popped in this step.
+    // A step in two halves around its one round of loads (r05: a cooperative wave-wide fetch in
+    // between lost 14-26 %, profiles/r05_coop_fetch_ab.txt; the split alone is neutral).
+    // step_begin: the state changes that need no global memory; returns the FETCH_Q float4 the
+    // step reads, or null once the query is finished (mode == TM_DONE).  fresh: a mesh node was
+    // popped in this step.
     template <bool SH>
     RT_D const float4* step_begin(const DevScene& sc, const Stack& st, bool& fresh) {
         // 1. state changes that need no global memory
@@ -1692,65 +1693,12 @@ constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 // VGPR budget.  The block's LDS (a 16-entry stack + the hit barycentrics, 34.8 KB) allows 4
 // blocks per CU, i.e. 4 trace waves per SIMD, whatever the registers.  The LDS is dynamic so
 // that the compiler does not see that cap and keeps the listed builds in a 5-wave budget:
-// 96 / 86 VGPRs without spills, which leaves room for two 64-VGPR k_shade waves beside four
+// 90 / 86 VGPRs without spills (r05: 96 before the step split), which leaves room for two 64-VGPR k_shade waves beside four
 // trace waves instead of one (the 112-VGPR build).  The top-level builds keep the 4-wave
 // budget (118 / 114 VGPRs; at 96 they spill).
-#ifndef RT_TRACE_STACK
-#define RT_TRACE_STACK 16
-#endif
-#ifndef RT_COOP
-#define RT_COOP 0
-#endif
-#ifndef RT_COOP_WAVES
-#define RT_COOP_WAVES 4
-#endif
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(RT_COOP ? RT_COOP_WAVES : LST ? 5 : 4)))
-constexpr int TRACE_STACK_LDS = RT_TRACE_STACK;      // stack levels in LDS (the rest spill to global)
-constexpr bool TRACE_COOP = RT_COOP != 0;            // cooperative step fetch (coop_fetch)
-constexpr size_t COOP_STAGE_Q = 8*(64 + 1);          // float4 per wave: 8 rows of 64 lanes + a 16-byte skew
-constexpr size_t TRACE_LDS = sizeof(uint2)*TRACE_STACK_LDS*TB + sizeof(float2)*TB +
-                             (TRACE_COOP ? sizeof(float4)*COOP_STAGE_Q*(TB/64) : 0);   // dynamic, per block
-
-// The cooperative step fetch: the wave loads its 64 lanes' FETCH_Q float4 (one 128-byte
-// step line each) 8 lanes per line, so each of its 8 wave-instructions touches 8 lines
-// instead of 64 (the per-lane gather moves ~1 lane-line per clock per CU whatever the
-// occupancy; 8 lanes per line straight into LDS moved 1.28-1.43x as many lines at 8-16 waves
-// per CU, tools/microbench_gather.hip).  Every lane of the wave must call it; a lane with
-// src == null fetches nothing (its F is garbage).
-//   Instruction i: lanes 8g..8g+7 load the line of owner L = (g & 1) | i << 1 | (g >> 1) << 4
-//   (its address by ds_bpermute), lane 8g+j its float4 j, with global_load_lds_dwordx4 into
-//   row i of the wave's stage (1 KB, lane-linear: lane l writes slot l).  Row i starts at
-//   i*(1 KB + 16 B).  Owner L reads its float4 m at row (L >> 1) & 7, slot 8g + m: one address
-//   per lane plus immediate offsets.  The 16 lanes of each ds_read_b128 lane group ({0-3,
-//   12-15, 20-27}, ...) hold every row twice with g of both parities, so with the rows' 16-byte
-//   skew they read 16 distinct 16-byte slots of a 256-byte bank row: conflict-free.
-constexpr uint32_t COOP_ROW_Q = 64 + 1;              // float4 per stage row, the skew included
-// A lane with no step (src null) has its loaders read `idle` instead: a valid line, so the
-// loads need no branch (their LDS slots are never read).
-RT_D void coop_fetch(const float4* src, const float4* idle, float4 (&F)[FETCH_Q], float4* stage) {
-    const uint32_t lane = __lane_id();
-    const uint64_t a = (uint64_t)(src ? src : idle);
-    const int alo = (int)(uint32_t)a, ahi = (int)(uint32_t)(a >> 32);
-    const uint32_t g = lane >> 3, j = lane & 7u;
-    const int own4 = (int)(4u*((g & 1u) | ((g >> 1) << 4)));      // 4 x the owner of instruction 0
-    uint32_t lo[8], hi[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {                                  // all 16 in flight together
-        lo[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(own4 + 8*i, alo);
-        hi[i] = (uint32_t)__builtin_amdgcn_ds_bpermute(own4 + 8*i, ahi);
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const float4* oa = reinterpret_cast<const float4*>((uint64_t)lo[i] | ((uint64_t)hi[i] << 32));
-        __builtin_amdgcn_global_load_lds(oa + j, stage + COOP_ROW_Q*i, 16, 0, 0);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0): the DMA has landed in LDS
-    __builtin_amdgcn_wave_barrier();
-    const float4* row = stage + COOP_ROW_Q*((lane >> 1) & 7u) + 8*((lane & 1u) | ((lane >> 4) << 1));
-#pragma unroll
-    for (int m = 0; m < FETCH_Q; ++m) F[m] = row[m];
-    __builtin_amdgcn_wave_barrier();
-}
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LST ? 5 : 4)))
+constexpr int TRACE_STACK_LDS = STACK_LDS;
+constexpr size_t TRACE_LDS = sizeof(uint2)*TRACE_STACK_LDS*TB + sizeof(float2)*TB;   // dynamic, per block
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
@@ -1762,10 +1710,9 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
     // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
     __builtin_amdgcn_s_setprio(1);
-    extern __shared__ uint2 trace_lds[];   // TRACE_LDS bytes: the stack, the barycentrics, the fetch stages
+    extern __shared__ uint2 trace_lds[];   // TRACE_LDS bytes: the stack, then the barycentrics
     StackT<TRACE_STACK_LDS> st;
     st.lds = trace_lds; st.spill = spill; st.bary = reinterpret_cast<float2*>(trace_lds + TRACE_STACK_LDS*TB);
-    float4* const stage = reinterpret_cast<float4*>(st.bary + TB) + COOP_STAGE_Q*(threadIdx.x / 64);
     st.lane = threadIdx.x; st.block = TB;
     st.gtid = blockIdx.x*TB + threadIdx.x; st.nthreads = gridDim.x*TB;
     __shared__ uint32_t qlen[NSHARD];
@@ -1838,31 +1785,9 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             idle = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;
-        if (!TRACE_COOP) {
-            if (active) {
-                for (int k = 0; k < STEPS_PER_REFILL; ++k) {
-                    if (!tr.step(sc, st)) { finish(); active = false; break; }
-                }
-            }
-        } else {
-            // the wave steps together: the fetch between a step's halves is cooperative
+        if (active) {
             for (int k = 0; k < STEPS_PER_REFILL; ++k) {
-                const unsigned long long act = __ballot(active);
-                if (!act) break;
-                const bool lds_only = __ballot(active && (tr.sp > TRACE_STACK_LDS - tr.PUSH_MAX || !(tr.cflags & 64u))) == 0ull;
-                const float4* src = nullptr;
-                bool fresh = false;
-                if (active) {
-                    src = lds_only ? tr.template step_begin<true>(sc, st, fresh) : tr.template step_begin<false>(sc, st, fresh);
-                    if (!src) { finish(); active = false; }
-                }
-                float4 F[FETCH_Q];
-                coop_fetch(src, sc.tris, F, stage);
-                if (src) {
-                    const bool more = lds_only ? tr.template step_end<true, true>(sc, st, F, fresh)
-                                               : tr.template step_end<false, false>(sc, st, F, fresh);
-                    if (!more) { finish(); active = false; }
-                }
+                if (!tr.step(sc, st)) { finish(); active = false; break; }
             }
         }
         tally.check(tr.acc);                            // every lane is here
