@@ -224,7 +224,7 @@ def main():
         os.makedirs(asset_dir, exist_ok=True)
     shard_mode = rt.abi.RT_SHARD_PASSES if args.shard_mode == "passes" else rt.abi.RT_SHARD_TILES
     stream = torch.cuda.current_stream(device)
-    from buas_pathtracer_amd.sharding import render_frame_sharded
+    from buas_pathtracer_amd.sharding import render_frame_sharded, timing_summary
 
     def setup(name, fw, fh, adir):
         scene, cam, st, fc, post = rt.load_preset(CONFIGS[name]["preset"], fw, fh, asset_dir=adir)
@@ -238,13 +238,14 @@ def main():
             return dev.render_device(cam, st, fc, fw, fh, buf.data_ptr(), stream=stream.cuda_stream,
                                      shard_index=shard_index, shard_count=shard_count)
 
-        def step():
+        def step(timing=None):
             accum.zero_()
             if args.shard_of > 1:                          # diagnostic: one rank's share of an N-rank frame
                 return render_shard(args.shard_index, args.shard_of, accum)
             # this rank's share into a zeroed frame buffer, the RCCL sum-reduce of it over xGMI into
             # rank 0, which adds it to its accumulation buffer
-            return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch, reduce=distributed)
+            return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch, reduce=distributed,
+                                        timing=timing)
         return scene, dev, st, post, accum, step
 
     scene, dev, st, post, accum, step = setup(args.config, w, h, asset_dir)
@@ -279,9 +280,10 @@ def main():
     if distributed:
         dist.barrier()
     torch.cuda.synchronize(device)
+    timing = {}                      # per-step render / reduce times of this rank (rank diagnostics)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        s = step()
+        s = step(timing)
         closest += s.closest_hit_rays
         shadow += s.shadow_rays
         samples += s.samples
@@ -307,6 +309,30 @@ def main():
     if distributed:
         dist.all_reduce(totals, op=dist.ReduceOp.SUM)
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    # Per-rank diagnostics (N > 1): each rank's frame (render) times, its framebuffer reduce times and
+    # its samples, gathered to rank 0 -- so a scaling shortfall reads as imbalance, tail or reduce.
+    ranks_info = None
+    if distributed:
+        tsum = timing_summary(timing)
+        fr, rd = tsum["render_ms"], tsum["reduce_ms"]
+        row = [min(fr), sum(fr) / len(fr), max(fr), (sum(rd) / len(rd)) if rd else 0.0, max(rd) if rd else 0.0,
+               float(samples), 1e3 * elapsed / args.steps]
+        table = torch.zeros((world, len(row)), dtype=torch.float64, device=red_dev)
+        table[rank] = torch.tensor(row, dtype=torch.float64, device=red_dev)
+        dist.all_reduce(table, op=dist.ReduceOp.SUM)
+        rows = table.cpu().tolist()
+        ranks_info = {
+            "world_size": dist.get_world_size(), "backend": dist.get_backend(),
+            "device_count": torch.cuda.device_count(),
+            "per_rank": [{"rank": r, "frame_ms": {"min": round(x[0], 3), "mean": round(x[1], 3), "max": round(x[2], 3)},
+                          "reduce_ms": {"mean": round(x[3], 3), "max": round(x[4], 3)},
+                          "samples": int(x[5]), "step_ms": round(x[6], 3)} for r, x in enumerate(rows)],
+            "frame_ms_max_over_ranks": round(max(x[2] for x in rows), 3),
+            "frame_ms_mean_over_ranks": round(sum(x[1] for x in rows) / world, 3),
+            "reduce_ms_mean_over_ranks": round(sum(x[3] for x in rows) / world, 3),
+            "note": "frame_ms: host wall time of rt_render_device per timed step (it returns once the rank's share "
+                    "is done on the GPU); reduce_ms: HIP events around the RCCL reduce on the render stream (gloo: "
+                    "host time of the staged host reduce); step_ms: the rank's own timed-region time per step"}
     tl = [float(x) for x in totals.tolist()]
     closest_all, shadow_all, samples_all, traced_all, traced_sh_all = tl[:5]
     nf = len(rt.abi.TRAVERSAL_FIELDS)
@@ -486,6 +512,7 @@ def main():
                                 "closest": {f: v // args.steps for f, v in trav_all[0].items()},
                                 "shadow": {f: v // args.steps for f, v in trav_all[1].items()}},
             "c4": c4,
+            "ranks": ranks_info,
             "cpu_baseline": cpu,
             "postprocess": postprocess,
         }

@@ -1172,7 +1172,12 @@ struct Pool {
     uint32_t* sh_dst;    // [N] the NEE term's destination (survivor's nx slot or SH_FIN | entry)
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
     uint32_t* free_n;    // [blocks]: the block's slots past its survivors, for the next k_generate (k_shade)
-    uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
+    // Claims in two levels (r05): blocks in groups of CLAIM_GROUP; k_shade adds its free count to its
+    // group's sum (one more atomic in its block tally), k_bookkeep scans the group sums (one wave), and
+    // k_generate block b claims from claim_base[b / CLAIM_GROUP] + the free counts of the blocks before
+    // it in its group (one coalesced load and a wave reduction).
+    uint32_t* group_sum; // [groups]: sum of the group's free_n (k_shade adds, k_bookkeep reads and zeroes)
+    uint32_t* claim_base;// [groups]: exclusive scan of group_sum (k_bookkeep) = first claim of the group
     PathOut nx;          // the other buffer: k_shade's survivors, k_connect's NEE terms for them
     // finished paths, per wave of 64 slots compacted from the wave's first entry (k_shade; the next
     // k_generate splats them, k_connect adds a pending last NEE term): {L, vignette}, {ray_d.w key,
@@ -1208,6 +1213,8 @@ constexpr uint32_t SH_FIN = 0x80000000u;   // Pool::sh_slot: the shadow ray's pa
 constexpr int NSHARD = 8;
 static_assert(NSHARD <= 64 && (NSHARD & (NSHARD - 1)) == 0, "k_bookkeep sums the shards in one wave");
 constexpr int NXCD = 8;                        // MI355X: workgroups are dealt round robin over 8 XCDs
+constexpr uint32_t CLAIM_GROUP = 64;           // k_shade / k_generate blocks per claim group (Pool::group_sum)
+static_assert(CLAIM_GROUP == 64, "k_generate sums a group's earlier blocks with one lane per block");
 constexpr int LINE_WORDS = 32;
 struct Counters {
     uint32_t ext_count[2][NSHARD][LINE_WORDS];   // extension queue length per shard (ping-pong)
@@ -1565,7 +1572,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += pool.free_w[wbase - wave + w];
     const bool want = lane >= first;
-    const uint32_t cbase = pool.claim_base[slot / BLOCK];
+    const uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot / BLOCK));
+    const uint32_t g0 = blk & ~(CLAIM_GROUP - 1u);
+    const uint32_t cbase = pool.claim_base[blk / CLAIM_GROUP] +
+                           __ockl_wfred_add_u32(g0 + lane < blk ? pool.free_n[g0 + lane] : 0u);
     const unsigned long long remaining = remaining_samples(cnt);
     const uint32_t claim = cbase + before + (lane - first);
     // No sample left for this block to claim (the frame's drain): its free slots go idle
@@ -2155,7 +2165,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     }
     const bool tp[6] = {enq, shadow, cont, cast_shadow, fin, slot < pool.n && !cont};
     uint32_t* const tc[6] = {&cnt->ext_count[nxt][shard][0], &cnt->shadow_count[shard][0], &cnt->alive[shard][0],
-                             &cnt->cast[1][shard][0], &cnt->unsplat[shard][0], nullptr};
+                             &cnt->cast[1][shard][0], &cnt->unsplat[shard][0], &pool.group_sum[blockIdx.x / CLAIM_GROUP]};
     uint32_t tpos[6], ttot[6];
     block_tally<BLOCK, 6>(tp, tc, tpos, ttot, tally);
     if (threadIdx.x == 0) {
@@ -2668,20 +2678,13 @@ enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
 // cast0: max_bounce_count > 0, so every sample claimed this iteration casts a camera ray (k_bookkeep counts
 // them from the claims; k_generate keeps no counter for them)
 struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0; };
-// Two workgroup sizes, picked per frame by the partition's pool (BK_LARGE_POOL): a pool of 4M paths or
-// more (a whole 1080p frame: 8.4M) takes the 512-thread build (92 VGPRs: 8 waves that find room beside
-// the other partitions' kernels sooner), a smaller one (a rank's share of a multi-GPU frame: 3.3M) the
-// 1024-thread build (62 VGPRs, 16 waves on one CU).  A/B (profiles/r03b_ab.txt section 14): 256 threads
-// (156 VGPRs) gave the full C3 frame +0.5 to +0.9 % and C4 +1.2 to +1.5 % over 1024, but rank 0 of 8
-// -1.9 to -2.8 %; with the 96-VGPR trace kernels 512 threads give C3 +1.5 to +2.2 % over 256 and C4 -0.1 to
-// -1.0 % (profiles/r04_bookkeep_ab.txt).
-constexpr int BK_THREADS_SMALL = 1024, BK_THREADS_LARGE = 512;
-constexpr uint32_t BK_LARGE_POOL = 4u << 20;
-template <int BK_THREADS>
+// One wave (r05).  It used to scan every block's free count itself (up to 32k, one workgroup of 512 or
+// 1024 threads): 32 us alone but 342 us beside the other partitions' kernels, a workgroup of 8-16 waves
+// waiting for room on one CU (9.5 % of C3's kernel time, profiles/r04_c3_pmc.md).  Now k_shade adds its
+// free count to its claim group's sum and this wave scans the group sums only (Pool::group_sum).
+constexpr int BK_THREADS = 64;
 __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
                                                          ResPlan plan) {
-    __shared__ uint32_t sc[BK_THREADS];
-    __shared__ uint32_t carry;
     const uint32_t t = threadIdx.x;
     if (phase == BK_FINAL) {
         if (t == 0) {
@@ -2691,144 +2694,137 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         }
         return;
     }
-    // The free counts' loads go out first, so they overlap the counter work below.
-    // Up to BK_EMAX entries per thread (pools up to 32k blocks, 8.4M paths) are loaded at once into
-    // registers, all in flight, and the claims are written from them; a loop covers larger pools.
-    constexpr uint32_t BK_EMAX = 32*(1024 / BK_THREADS);
-    const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
-    const uint32_t lo = t*E, hi = min(lo + E, nblocks);
+    // The group sums' loads go out first, so they overlap the counter work below: lane t owns the
+    // contiguous groups [t*E, t*E + E), up to BK_EMAX of them in registers (pools up to 32M paths).
+    constexpr uint32_t BK_EMAX = 32;
+    const uint32_t ngroups = (nblocks + CLAIM_GROUP - 1) / CLAIM_GROUP;
+    const uint32_t E = (ngroups + BK_THREADS - 1) / BK_THREADS;
+    const uint32_t lo = t*E, hi = min(lo + E, ngroups);
     uint32_t v[BK_EMAX];
     if (E <= BK_EMAX) {
 #pragma unroll
-        for (uint32_t j = 0; j < BK_EMAX; ++j) v[j] = lo + j < hi ? pool.free_n[lo + j] : 0u;
+        for (uint32_t j = 0; j < BK_EMAX; ++j) {
+            const uint32_t g = lo + j;
+            // before the first iteration every block is free (free_n = BLOCK, set by the host)
+            v[j] = g >= hi ? 0u : phase == BK_FIRST ? (min(nblocks - g*CLAIM_GROUP, CLAIM_GROUP)*BLOCK)
+                                                    : pool.group_sum[g];
+        }
     }
-    __shared__ uint32_t skip;
-    if (t < 64) {
-        // Lane k < NSHARD reads shard k's counters, all loads in flight, and the sums come from
-        // shuffles.  (Thread 0 alone walking the shards, each load ordered behind the previous
-        // shard's stores, took ~60 dependent round trips: 27 us alone, ~290 us beside the other
-        // partitions' kernels, 10 % of a partition's iteration.)
-        const bool it_phase = phase == BK_ITER;
-        const uint32_t done_flag = it_phase ? cnt->done : 0u;
-        uint32_t al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
-        if (it_phase && t < NSHARD) {
-            al = cnt->alive[t][0];
-            c1 = cnt->cast[1][t][0];
-            us = cnt->unsplat[t][0];
-            eq = cnt->ext_count[cur][t][0];
-            sq = cnt->shadow_count[t][0];
-        }
-        unsigned long long next = 0, total = 0, lim = 0, start = 0;
-        uint32_t gfree = 0, it = 0, rcur = 0;
-        if (t == 0 && it_phase) {
-            next = cnt->next_sample; total = cnt->total_samples; lim = cnt->claim_limit;
-            start = cnt->start_sample; gfree = cnt->gen_free; it = cnt->iter; rcur = cnt->res_cursor;
-        }
-        // the claim cursor `life` iterations ago (loaded before any store to the counters)
-        const unsigned long long done_cursor =
-            (t == 0 && it_phase && plan.mode && it >= plan.life) ? cnt->hist[(it - plan.life) & 127u] : start;
-        const bool sk = it_phase && done_flag;
-        if (it_phase && !sk && t < NSHARD) {
-            cnt->unsplat[t][0] = 0;
-            cnt->cast[1][t][0] = 0;
-            cnt->alive[t][0] = 0;
-            cnt->ext_count[cur][t][0] = 0;
-            cnt->shadow_count[t][0] = 0;
-            cnt->fetch[0][t][0] = 0;
-            cnt->fetch[1][t][0] = 0;
-        }
-        uint32_t ext = al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
+    // Lane k < NSHARD reads shard k's counters, all loads in flight, and the sums come from
+    // shuffles.  (Thread 0 alone walking the shards, each load ordered behind the previous
+    // shard's stores, took ~60 dependent round trips: 27 us alone, ~290 us beside the other
+    // partitions' kernels, 10 % of a partition's iteration.)
+    const bool it_phase = phase == BK_ITER;
+    const uint32_t done_flag = it_phase ? cnt->done : 0u;
+    uint32_t al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
+    if (it_phase && t < NSHARD) {
+        al = cnt->alive[t][0];
+        c1 = cnt->cast[1][t][0];
+        us = cnt->unsplat[t][0];
+        eq = cnt->ext_count[cur][t][0];
+        sq = cnt->shadow_count[t][0];
+    }
+    unsigned long long next = 0, total = 0, lim = 0, start = 0;
+    uint32_t gfree = 0, it = 0, rcur = 0;
+    if (t == 0 && it_phase) {
+        next = cnt->next_sample; total = cnt->total_samples; lim = cnt->claim_limit;
+        start = cnt->start_sample; gfree = cnt->gen_free; it = cnt->iter; rcur = cnt->res_cursor;
+    }
+    // the claim cursor `life` iterations ago (loaded before any store to the counters)
+    const unsigned long long done_cursor =
+        (t == 0 && it_phase && plan.mode && it >= plan.life) ? cnt->hist[(it - plan.life) & 127u] : start;
+    const bool sk = it_phase && done_flag;
+    if (it_phase && !sk && t < NSHARD) {
+        cnt->unsplat[t][0] = 0;
+        cnt->cast[1][t][0] = 0;
+        cnt->alive[t][0] = 0;
+        cnt->ext_count[cur][t][0] = 0;
+        cnt->shadow_count[t][0] = 0;
+        cnt->fetch[0][t][0] = 0;
+        cnt->fetch[1][t][0] = 0;
+    }
+    uint32_t ext = al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
 #pragma unroll
-        for (int off = 1; off < NSHARD; off <<= 1) {
-            ext += __shfl_xor(ext, off); sh += __shfl_xor(sh, off); pend += __shfl_xor(pend, off);
-            ps += __shfl_xor(ps, off); tq += __shfl_xor(tq, off); ts += __shfl_xor(ts, off);
+    for (int off = 1; off < NSHARD; off <<= 1) {
+        ext += __shfl_xor(ext, off); sh += __shfl_xor(sh, off); pend += __shfl_xor(pend, off);
+        ps += __shfl_xor(ps, off); tq += __shfl_xor(tq, off); ts += __shfl_xor(ts, off);
+    }
+    if (t == 0) {
+        if (sk) {
+            // done: the passes the bookkeep that found it complete could not plan (an iteration
+            // without a resolve after it) are resolved after this one, on the device, instead of
+            // waiting for the host's BK_FINAL
+            const bool last = plan.mode && rcur < plan.pass1;
+            cnt->res_from = last ? rcur : 0u;
+            cnt->res_to = last ? plan.pass1 : 0u;
+            if (last) cnt->res_cursor = plan.pass1;
         }
-        if (t == 0) {
-            skip = sk;
-            if (sk) {
-                // done: the passes the bookkeep that found it complete could not plan (an iteration
-                // without a resolve after it) are resolved after this one, on the device, instead of
-                // waiting for the host's BK_FINAL
-                const bool last = plan.mode && rcur < plan.pass1;
-                cnt->res_from = last ? rcur : 0u;
-                cnt->res_to = last ? plan.pass1 : 0u;
-                if (last) cnt->res_cursor = plan.pass1;
-            }
-            if (it_phase && !sk) {
-                const unsigned long long lm = lim < total ? lim : total;
-                const unsigned long long rem = lm > next ? lm - next : 0ull;      // remaining_samples()
-                const unsigned long long claimed = (unsigned long long)gfree < rem ? (unsigned long long)gfree : rem;
-                next += claimed;
-                cnt->next_sample = next;
-                // the camera rays of this iteration's k_generate: one per claimed sample (every claim below
-                // the remaining count becomes a path, k_generate) when max_bounce_count > 0
-                cnt->closest_rays += ext + (plan.cast0 ? claimed : 0ull);
-                cnt->shadow_rays += sh;
-                cnt->traced_rays[0] += tq;
-                cnt->traced_rays[1] += ts;
-                cnt->pending = pend;
-                cnt->pending_splat = ps;
-                // nothing left to claim, trace or splat: every record is in the ring
-                const bool complete = next >= total && pend == 0 && ps == 0;
-                if (complete) cnt->done = 1;
-                else if (plan.fuse && next >= total && pend <= plan.fuse) cnt->fused = 1;
-                cnt->iter = it + 1;
-                cnt->hist[it & 127u] = next;
-                if (plan.mode) {
-                    const uint32_t done_pass = complete ? plan.pass1 : (uint32_t)(done_cursor / plan.P);
-                    const uint32_t from = rcur;
-                    cnt->res_from = cnt->res_to = 0;
-                    if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
-                        cnt->res_from = from;
-                        cnt->res_to = done_pass;
-                        cnt->res_cursor = done_pass;
-                        // the ring slots of [from, done_pass) are free once the resolve launched next has run
-                        cnt->claim_limit = (unsigned long long)(done_pass + plan.ring)*plan.P;
-                    }
+        if (it_phase && !sk) {
+            const unsigned long long lm = lim < total ? lim : total;
+            const unsigned long long rem = lm > next ? lm - next : 0ull;      // remaining_samples()
+            const unsigned long long claimed = (unsigned long long)gfree < rem ? (unsigned long long)gfree : rem;
+            next += claimed;
+            cnt->next_sample = next;
+            // the camera rays of this iteration's k_generate: one per claimed sample (every claim below
+            // the remaining count becomes a path, k_generate) when max_bounce_count > 0
+            cnt->closest_rays += ext + (plan.cast0 ? claimed : 0ull);
+            cnt->shadow_rays += sh;
+            cnt->traced_rays[0] += tq;
+            cnt->traced_rays[1] += ts;
+            cnt->pending = pend;
+            cnt->pending_splat = ps;
+            // nothing left to claim, trace or splat: every record is in the ring
+            const bool complete = next >= total && pend == 0 && ps == 0;
+            if (complete) cnt->done = 1;
+            else if (plan.fuse && next >= total && pend <= plan.fuse) cnt->fused = 1;
+            cnt->iter = it + 1;
+            cnt->hist[it & 127u] = next;
+            if (plan.mode) {
+                const uint32_t done_pass = complete ? plan.pass1 : (uint32_t)(done_cursor / plan.P);
+                const uint32_t from = rcur;
+                cnt->res_from = cnt->res_to = 0;
+                if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
+                    cnt->res_from = from;
+                    cnt->res_to = done_pass;
+                    cnt->res_cursor = done_pass;
+                    // the ring slots of [from, done_pass) are free once the resolve launched next has run
+                    cnt->claim_limit = (unsigned long long)(done_pass + plan.ring)*plan.P;
                 }
             }
-            carry = 0;
         }
     }
-    __syncthreads();
-    if (skip) return;
-    // exclusive scan of free_n: thread t owns the contiguous entries [t*E, t*E + E), sums them,
-    // then a wave scan by shuffles and one barrier for the 16 wave totals.
-    // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
-    // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
+    if (sk) return;                                    // uniform
+    // exclusive scan of the group sums: lane t sums its groups, a wave scan by shuffles; the group
+    // sums are zeroed for the next k_shade (which runs after the k_generate that reads claim_base)
     uint32_t sum = 0;
     if (E <= BK_EMAX) {
 #pragma unroll
         for (uint32_t j = 0; j < BK_EMAX; ++j) sum += v[j];
     } else {
-        for (uint32_t i = lo; i < hi; ++i) sum += pool.free_n[i];
+        for (uint32_t g = lo; g < hi; ++g)
+            sum += phase == BK_FIRST ? min(nblocks - g*CLAIM_GROUP, CLAIM_GROUP)*BLOCK : pool.group_sum[g];
     }
-    const uint32_t lane = t & 63u, wave = t >> 6;
     uint32_t incl = sum;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t u = __shfl_up(incl, off);
-        if (lane >= (uint32_t)off) incl += u;
+        if (t >= (uint32_t)off) incl += u;
     }
-    if (lane == 63) sc[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0;
-    for (uint32_t w = 0; w < wave; ++w) before += sc[w];
-    uint32_t run = before + incl - sum;
+    uint32_t run = incl - sum;
     if (E <= BK_EMAX) {
 #pragma unroll
         for (uint32_t j = 0; j < BK_EMAX; ++j)
-            if (lo + j < hi) { pool.claim_base[lo + j] = run; run += v[j]; }
+            if (lo + j < hi) { pool.claim_base[lo + j] = run; pool.group_sum[lo + j] = 0u; run += v[j]; }
     } else {
-        for (uint32_t i = lo; i < hi; ++i) {
-            const uint32_t x = pool.free_n[i];
-            pool.claim_base[i] = run;
+        for (uint32_t g = lo; g < hi; ++g) {
+            const uint32_t x = phase == BK_FIRST ? min(nblocks - g*CLAIM_GROUP, CLAIM_GROUP)*BLOCK : pool.group_sum[g];
+            pool.claim_base[g] = run;
+            pool.group_sum[g] = 0u;
             run += x;
         }
     }
-    if (t == BK_THREADS - 1) carry = run;
-    __syncthreads();
-    if (t == 0) cnt->gen_free = carry;
+    const uint32_t all = __shfl(incl, 63);
+    if (t == 0) cnt->gen_free = all;
 }
 
 // debug / parity kernel: intersect_scene / intersect_shadow_ray for explicit rays,
@@ -3187,7 +3183,9 @@ int ensure_pool(Partition& pt, uint32_t n) {
     const size_t Q = cap*NSHARD;
     p.shard_cap = (uint32_t)cap;
     e |= alloc((void**)&p.free_n, 4*nblocks);
-    e |= alloc((void**)&p.claim_base, 4*nblocks);
+    const size_t ngroups = (nblocks + CLAIM_GROUP - 1) / CLAIM_GROUP;
+    e |= alloc((void**)&p.claim_base, 4*ngroups);
+    e |= alloc((void**)&p.group_sum, 4*ngroups);
     e |= alloc((void**)&p.fin_w, 4*(N / 64));
     e |= alloc((void**)&p.free_w, 4*(N / 64));
     e |= alloc((void**)&p.fin_L, 16*N);
@@ -3320,12 +3318,9 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     const FrameShape shape = frame_shape(s, total, listed ? 0u : sp.passes);
     const int nparts = shape.nparts;
     const uint32_t pool_n = shape.pool_n;
-    // k_bookkeep's workgroup size by the pool (BK_LARGE_POOL, see k_bookkeep)
-    const bool bk_large = pool_n >= BK_LARGE_POOL;
-    auto launch_bookkeep = [bk_large](Counters* c, const Pool& pl, uint32_t nblocks, int cur, int phase, ResPlan plan,
-                                      hipStream_t q) {
-        if (bk_large) k_bookkeep<BK_THREADS_LARGE><<<1, BK_THREADS_LARGE, 0, q>>>(c, pl, nblocks, cur, phase, plan);
-        else k_bookkeep<BK_THREADS_SMALL><<<1, BK_THREADS_SMALL, 0, q>>>(c, pl, nblocks, cur, phase, plan);
+    auto launch_bookkeep = [](Counters* c, const Pool& pl, uint32_t nblocks, int cur, int phase, ResPlan plan,
+                              hipStream_t q) {
+        k_bookkeep<<<1, BK_THREADS, 0, q>>>(c, pl, nblocks, cur, phase, plan);
     };
     const bool stream_splat = !listed && sp.mode == RT_SPLAT_STREAM;
     const size_t npx = (size_t)fp.w*fp.h;
@@ -3393,6 +3388,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + 2, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
+        // (the group sums are zeroed by the BK_FIRST bookkeep below, which scans the all-free pool)
         HIP_OK(hipMemsetAsync(pt.pool.fin_w, 0, 4ull*N / 64, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_w, 64, N / 64, r.stream));
         launch_bookkeep(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{}, r.stream);

@@ -216,7 +216,10 @@ enum rt_kernel_id {                 /* wavefront stages, for rt_stats::kernel_ms
  *   - mesh BVHs are BVH4s (each BVH2 interior node merged with its interior children), and a child
  *     is box-tested when its parent is expanded instead of when it is popped.
  * A shadow query that a mesh occludes is counted like any other (the reference returns before its
- * traversal counts are added, RT/intersection.cpp:297-299). */
+ * traversal counts are added, RT/intersection.cpp:297-299).
+ * So these values are NOT comparable to the reference's own TraversalStats for the same frame (C3:
+ * mesh_bvh_traversals 3.6 G BVH4 steps against the reference's 10.4 G BVH2 pops); tests pin them
+ * against the oracle's restatement of this library's walk (tests/test_gpu_fullscale.py). */
 typedef struct rt_traversal_stats {
     /* intersect_mesh calls (RT/intersection.cpp:488, counted at :254): mesh instances a query's
        top-level walk reaches -- the top-level leaf holding the instance passes its pop-time test
@@ -464,7 +467,7 @@ typedef struct rt_scene_config {
     int32_t  splat_ring;            /* streaming splat: record-ring passes per partition; 0 = auto   */
     double   sample_budget_gb;      /* HBM for sample records; < 0 = auto (free HBM less 16 GB)      */
     int64_t  resolve_tall_pixels;   /* exact splat: 8-row gather strips from this many pixels; 0 = auto */
-    int32_t  debug_traversal;       /* 1: longest-traversal diagnostics to stderr                   */
+    int32_t  debug_traversal;       /* 1: each frame's TraversalStats and trace steps to stderr      */
     int32_t  reserved[7];
 } rt_scene_config;
 int rt_scene_default_config(rt_scene_config* out);

@@ -811,6 +811,22 @@ static int gw_top(const rt_scene_desc* sc, const Ray* ray, const int neg[3], int
     return 0;
 }
 
+/* Whether the library's ray prologue walks this top level: top_sequences (rt_kernels.hip) builds
+ * its per-octant sequences only for at most 255 nodes and 63 bvh_indices slots, and gives up on a
+ * node index out of range, a walk deeper than 64, or a leaf of more than 127 primitives or past the
+ * slots; then the trace kernels walk the whole top level.  The same checks, on octant 0's order
+ * (every octant visits the same nodes). */
+static int gw_top_node_ok(const rt_scene_desc* sc, uint32_t n, uint32_t depth) {
+    if (n >= sc->bvh_node_count || depth > 64) return 0;
+    const rt_bvh_node* nd = &sc->bvh_nodes[n];
+    if (nd->count) return nd->count <= 127 && nd->left_first + nd->count <= sc->bvh_index_count;
+    if (nd->left_first == 0 || nd->left_first + 1 >= sc->bvh_node_count || nd->split_axis > 2) return 1;
+    return gw_top_node_ok(sc, nd->left_first, depth + 1) && gw_top_node_ok(sc, nd->left_first + 1, depth + 1);
+}
+static int gw_top_prologue(const rt_scene_desc* sc) {
+    return sc->bvh_node_count && sc->bvh_node_count <= 255 && sc->bvh_index_count <= 63 && gw_top_node_ok(sc, 0, 0);
+}
+
 static void gpu_walk_query(const rt_scene_desc* sc, const Ray* ray, int occ, uint32_t ignored, uint64_t* g) {
     float t = ray->max_t;
     for (uint32_t i = 0; i < sc->plane_count; ++i) {                  /* the planes first */
@@ -819,7 +835,7 @@ static void gpu_walk_query(const rt_scene_desc* sc, const Ray* ray, int occ, uin
     }
     if (!sc->bvh_node_count) return;
     /* the prologue walks the top level when it fits its tables (top_sequences, rt_kernels.hip) */
-    if (g_gw_top && sc->bvh_node_count <= 255 && sc->bvh_index_count <= 63) {
+    if (g_gw_top && gw_top_prologue(sc)) {
         static const int oct0[3] = {0, 0, 0};
         uint32_t list[64], n = 0;
         if (gw_top(sc, ray, oct0, occ, ignored, &t, list, &n, g, 0)) return;

@@ -42,6 +42,21 @@ def _run(cmd, env):
     return json.loads(lines[0])
 
 
+def _check_ranks(out, world, backend):
+    """bench.py's per-rank diagnostics (N > 1 / --force-dist): the world RCCL / gloo formed, the
+    devices visible, and per rank its frame (render) and framebuffer-reduce times and its samples."""
+    r = out["ranks"]
+    assert r["world_size"] == world and r["backend"] == backend and r["device_count"] >= 1
+    assert [x["rank"] for x in r["per_rank"]] == list(range(world))
+    for x in r["per_rank"]:
+        fm = x["frame_ms"]
+        assert 0 < fm["min"] <= fm["mean"] <= fm["max"]
+        assert 0 <= x["reduce_ms"]["mean"] <= x["reduce_ms"]["max"]
+        assert x["samples"] > 0 and x["step_ms"] >= fm["mean"]
+    assert r["frame_ms_max_over_ranks"] == max(x["frame_ms"]["max"] for x in r["per_rank"])
+    assert out["ms_per_step"] >= r["frame_ms_mean_over_ranks"]
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_match_one(tmp_path):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
@@ -62,6 +77,11 @@ def test_bench_two_ranks_match_one(tmp_path):
         assert k in two, k
     assert two["n_gpus"] == 2 and one["n_gpus"] == 1
     assert two["config"]["parallelism"] == "passes%2+gloo_reduce"
+    _check_ranks(two, 2, "gloo")
+    assert one["ranks"] is None
+    # the per-rank samples add up to the one-rank frame's
+    assert sum(r["samples"] for r in two["ranks"]["per_rank"]) == \
+        pytest.approx(one["samples_per_s"] * one["ms_per_step"] / 1e3 * two["steps"], rel=1e-3)
     for k in ("closest_hit_rays", "shadow_rays", "traced_rays"):
         assert two[k] == one[k], k
     assert two["samples_per_s"] * two["ms_per_step"] == pytest.approx(one["samples_per_s"] * one["ms_per_step"], rel=1e-3)
@@ -86,6 +106,8 @@ def test_bench_rccl_one_rank(tmp_path):
                                      "parallelism": rccl["config"]["parallelism"]}
     assert rccl["config"]["parallelism"] == "passes%1+rccl_reduce"
     assert rccl["n_gpus"] == plain["n_gpus"] == 1
+    _check_ranks(rccl, 1, "nccl")
+    REPORT["bench_rccl_one_rank"]["ranks"] = rccl["ranks"]
     for k in ("closest_hit_rays", "shadow_rays", "traced_rays", "traversal_stats"):
         assert rccl[k] == plain[k], k
     assert (rccl["c4"]["closest_hit_rays"], rccl["c4"]["shadow_rays"]) == (plain["c4"]["closest_hit_rays"],

@@ -65,9 +65,15 @@ def _worker(rank, world, port, out_path, backend):
         return stats.samples
 
     samples = 0
+    timing = {}
     for f in range(2):                      # two progressive frames (RT/raytracer.cpp:720-724)
         frame["fc"], frame["tfi"] = f * SPP, f
-        samples += render_frame_sharded(render_shard, accum, rank, world)
+        samples += render_frame_sharded(render_shard, accum, rank, world, timing=timing)
+    # the per-rank diagnostics bench.py reports for N > 1: one render and one reduce time per frame
+    from buas_pathtracer_amd.sharding import timing_summary
+    ts = timing_summary(timing)
+    assert len(ts["render_ms"]) == 2 and len(ts["reduce_ms"]) == 2
+    assert all(t > 0 for t in ts["render_ms"]) and all(t >= 0 for t in ts["reduce_ms"])
     n = torch.tensor([samples], dtype=torch.float64)
     dist.all_reduce(n)
     if rank == 0:

@@ -5,7 +5,8 @@ bench's frames run: four partitions, 8.4M-path pools, the streaming splat's reco
 chunks, the fused drain -- against the oracle's frame of the same samples (RT_RNG_PER_SAMPLE, the
 reference-order splat, RT/raytracer.cpp:366-495, :692-757):
 
-* C3 (1920x1080, 256 spp) and C4 (1920x1080, 256 spp, ~250k triangles): the whole frame, rel L2
+* C2 (1920x1080, 64 spp, r05), C3 (1920x1080, 256 spp) and C4 (1920x1080, 256 spp, ~250k
+  triangles): the whole frame, rel L2
   <= 1e-5 (the streaming splat sums a pixel pass by pass, the reference tile by tile) and the same
   closest-hit and shadow ray counts, call for call;
 * the frame's TraversalStats (rt_stats::traversal, RT/intersection.h:33-40): the GPU counts its own
@@ -47,11 +48,11 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
 
 
-@pytest.mark.parametrize("preset", ["c3", "c4"])
-def test_full_frame_default_path(rt, preset):
+@pytest.mark.parametrize("preset,spp", [("c2", 64), ("c3", 256), ("c4", 256)])
+def test_full_frame_default_path(rt, preset, spp):
     w, h = 1920, 1080
     scene, cam, st, fc, post = rt.load_preset(preset, w, h)
-    assert st.samples_per_pixel == 256
+    assert st.samples_per_pixel == spp
     dev = rt.DeviceScene(scene, 0)
     try:
         gpu, gs = dev.render(cam, st, fc, w, h)
@@ -63,12 +64,12 @@ def test_full_frame_default_path(rt, preset):
         cpu, cs = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=threads)
     err = rel_l2(gpu, cpu)
     trav = traversal_report(gs, cs, walk.result)
-    REPORT[f"fullscale_{preset}_1080p_256spp"] = {
+    REPORT[f"fullscale_{preset}_1080p_{spp}spp"] = {
         "rel_l2": err, "max_abs_weight_diff": float(np.abs(gpu[..., 3] - cpu[..., 3]).max()),
         "gpu_rays": [int(gs.closest_hit_rays), int(gs.shadow_rays)], "oracle_rays": [int(cs.closest_hit_rays), int(cs.shadow_rays)],
         "samples": int(gs.samples), "iterations": int(gs.iterations), "oracle_threads": threads,
         "gpu_seconds": gs.seconds, "traversal": trav}
-    assert gs.samples == cs.samples == w * h * 256
+    assert gs.samples == cs.samples == w * h * spp
     assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
     assert np.isfinite(gpu).all() and np.isfinite(cpu).all()
     assert err <= 1e-5

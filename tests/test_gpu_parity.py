@@ -217,7 +217,8 @@ def test_stream_splat_vs_reference_order(which, w, h, request):
     REPORT[f"frame_stream_{which}"] = {"rel_l2": err, "max_abs_weight_diff": wdiff}
     assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
     assert err <= 1e-5
-    assert np.isfinite(gpu).all() == np.isfinite(cpu).all()
+    assert np.isfinite(gpu).all()
+    assert np.isfinite(cpu).all()
 
 
 @pytest.mark.parametrize("env", [{"splat_chunk": 1, "splat_ring": 1}, {"splat_chunk": 3, "splat_ring": 5},

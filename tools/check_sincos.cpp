@@ -1,6 +1,6 @@
 // Host check that d_sincosf(x) gives exactly d_sinf(x) and d_cosf(x), bit for bit, for every float
 // (the device math is plain IEEE f32 without contraction, so the host build computes the same bits).
-//   g++ -O2 -ffp-contract=off -DRT_DMATH_HOST_TEST -DRT_RCP_CR=0 -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
+//   g++ -O2 -ffp-contract=off -DRT_DMATH_HOST_TEST -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ \
 //       tools/check_sincos.cpp -o /tmp/check_sincos && /tmp/check_sincos
 #include <cstdio>
 #include <cstring>
