@@ -417,7 +417,7 @@ def main():
         traversal = None
         if args.warmup:
             traversal = {"peak": L2_PEAK_GBS, "unit": "GB/s", "bytes_per_step": 128,
-                         "source": "rt_stats::trace_steps of the timed frames (counted on the device)",
+                         "source": "rt_stats::trace_steps of the timed frames (counted on the device; the extend / connect launches' own steps, the fused drain's left out)",
                          "timing": "warm-up frames, HIP events on each partition's stream (shared GPU)"}
             for kind, (stage, kname, rays) in enumerate((("extend", "k_extend", traced), ("connect", "k_connect", traced_sh))):
                 k = STAGES.index(stage)

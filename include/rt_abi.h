@@ -256,8 +256,9 @@ typedef struct rt_stats {
     /* TraversalStats of the frame (above) per query kind: [0] closest-hit (intersect_scene),
        [1] shadow (intersect_shadow_ray); the reference's totals are the sums of the two */
     rt_traversal_stats traversal[2];
-    /* trace steps per kind (every step of the extend / connect kernels and the fused drain,
-       top-level steps included): the fetch rounds of 128 B per lane the traversal roofline counts */
+    /* trace steps per kind of the extend / connect kernels (top-level steps included; r05: the fused
+       drain's steps, which the TraversalStats above include, are left out, so that the steps match the
+       launches bench.py times): the fetch rounds of 128 B per lane the traversal roofline counts */
     uint64_t trace_steps[2];
 } rt_stats;
 

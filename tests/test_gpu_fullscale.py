@@ -107,7 +107,9 @@ def check_traversal(gs, walk):
                        ("mesh_bvh_traversals", "bvh")):
             g, r = getattr(t, f), walk[key][k]
             assert abs(g - r) <= 1e-6 * r, (k, f, g, r)
-        assert gs.trace_steps[k] >= t.mesh_bvh_traversals
+        # the extend / connect launches' steps: the fused drain's are in the counts but not in
+        # trace_steps (r05; every BASELINE scene is walked from the prologue's mesh lists: no top steps)
+        assert 0 < gs.trace_steps[k] <= t.mesh_bvh_traversals
 
 
 def test_c5_tile_shard_exact(rt):
