@@ -1177,12 +1177,7 @@ struct Pool {
     uint32_t* sh_dst;    // [N] the NEE term's destination (survivor's nx slot or SH_FIN | entry)
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
     uint32_t* free_n;    // [blocks]: the block's slots past its survivors, for the next k_generate (k_shade)
-    // Claims in two levels (r05): blocks in groups of CLAIM_GROUP; k_shade adds its free count to its
-    // group's sum (one more atomic in its block tally), k_bookkeep scans the group sums (one wave), and
-    // k_generate block b claims from claim_base[b / CLAIM_GROUP] + the free counts of the blocks before
-    // it in its group (one coalesced load and a wave reduction).
-    uint32_t* group_sum; // [groups]: sum of the group's free_n (k_shade adds, k_bookkeep reads and zeroes)
-    uint32_t* claim_base;// [groups]: exclusive scan of group_sum (k_bookkeep) = first claim of the group
+    uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
     PathOut nx;          // the other buffer: k_shade's survivors, k_connect's NEE terms for them
     // finished paths, per wave of 64 slots compacted from the wave's first entry (k_shade; the next
     // k_generate splats them, k_connect adds a pending last NEE term): {L, vignette}, {ray_d.w key,
@@ -1218,8 +1213,6 @@ constexpr uint32_t SH_FIN = 0x80000000u;   // Pool::sh_slot: the shadow ray's pa
 constexpr int NSHARD = 8;
 static_assert(NSHARD <= 64 && (NSHARD & (NSHARD - 1)) == 0, "k_bookkeep sums the shards in one wave");
 constexpr int NXCD = 8;                        // MI355X: workgroups are dealt round robin over 8 XCDs
-constexpr uint32_t CLAIM_GROUP = 64;           // k_shade / k_generate blocks per claim group (Pool::group_sum)
-static_assert(CLAIM_GROUP == 64, "k_generate sums a group's earlier blocks with one lane per block");
 constexpr int LINE_WORDS = 32;
 struct Counters {
     uint32_t ext_count[2][NSHARD][LINE_WORDS];   // extension queue length per shard (ping-pong)
@@ -1242,52 +1235,19 @@ struct Counters {
     // TraversalStats of the frame (rt_stats::traversal), per ray kind (0 closest, 1 shadow): TV_* counts,
     // one 128-byte line per shard (the block's or wave's shard adds to it; the host sums the shards)
     unsigned long long trav[NSHARD][2*TV_N];
-    // the frame's claim cursor and end as this partition's last bookkeep saw them (FrameShared; the
-    // host's termination test reads them with the counters)
     unsigned long long next_sample;
     unsigned long long total_samples;
     unsigned long long closest_rays;
     unsigned long long shadow_rays;
     unsigned long long traced_rays[2];   // handed to k_trace<false> / k_trace<true>
-    // the samples the next k_generate claims: [claim_start, claim_start + claim_n), reserved from the
-    // frame's queue by the bookkeep before it (FrameShared)
-    unsigned long long claim_start;
-    uint32_t claim_n;
+    // streaming splat (k_bookkeep plans, k_resolve_tiles consumes)
+    unsigned long long claim_limit;      // samples below this may be claimed: the record ring's capacity
+    unsigned long long start_sample;     // the partition's first sample
     uint32_t iter;                       // iterations bookkept so far
-    uint32_t res_from, res_to;           // the pass range this partition's next k_resolve_tiles resolves (empty: none)
-    // the lowest key (sample pass, or list index) of the paths k_shade processed this iteration (alive
-    // or finished, not yet splatted), per shard on a line of its own: k_shade's waves take the minimum,
-    // k_bookkeep reads it (a sample number: key * P, or the list index) and resets it (FrameShared::low)
-    uint32_t low_live[NSHARD][LINE_WORDS];
+    uint32_t res_cursor;                 // passes below it are resolved (or planned for the next resolve)
+    uint32_t res_from, res_to;           // the pass range the next k_resolve_tiles resolves (empty: none)
+    unsigned long long hist[128];        // next_sample after the bookkeep of iteration i, at [i % 128]
 };
-
-// The frame's shared claim queue and resolve plan (r05).  The reference's workers pull 64x64 tiles
-// from one atomic counter until none are left (RT/raytracer.cpp:551-560), so every worker stays busy
-// to the end.  Here the partitions' bookkeeps reserve their next k_generate's samples from one cursor
-// (compare-and-swap) in the same way, so the partitions run out of work together instead of each at
-// the end of a fixed range (r04: a rank's share of 8 ended its four partitions 1.5 ms apart, their
-// fused drains one after another).  The samples keep their keys, so who renders a sample changes
-// nothing in it; the streaming splat's records live in ONE ring indexed by the sample pass, and the
-// passes are resolved into the caller's buffer strictly in pass order, one resolve at a time (busy
-// flag): the frame's float sums do not depend on the partitions, their number or the timing.
-//   Completion: partition k publishes low[k], a sample below which it has nothing in flight (the
-//   lowest sample of the paths its last k_shade processed, Counters::low_live, and its reservation;
-//   ~0 when it holds nothing), BEFORE it moves the cursor; a planner reads the cursor (acquire) and
-//   then the lows: every sample below their minimum is splatted, so the passes below it may be
-//   resolved.
-struct FrameShared {
-    unsigned long long next_sample;      // the claim cursor
-    unsigned long long total_samples;    // the frame's end
-    unsigned long long claim_limit;      // samples below it may be claimed: the record ring's capacity
-    unsigned long long pad0[13];
-    unsigned long long low[16];          // per partition (MAX_PARTITIONS): nothing in flight below it (~0: none)
-    uint32_t res_cursor;                 // passes below it are resolved or being resolved
-    uint32_t res_busy;                   // 1 from a resolve's planning to its last block
-    uint32_t res_blocks;                 // blocks of the running resolve that are done
-    uint32_t ring;                       // the record ring's passes (streaming splat)
-    uint32_t pad1[28];
-};
-static_assert(sizeof(FrameShared) % 128 == 0 && offsetof(FrameShared, low) == 128, "FrameShared lines");
 
 struct FrameParams {
     uint32_t w, h, frame_count, total_frame_index;
@@ -1316,7 +1276,6 @@ struct FrameParams {
     float*  samp_jy;                // [spp*P]: jitter_y
     const int32_t* tile_base;       // [tiles]: first tile-list pixel of an owned tile, -1 otherwise
     uint32_t spp;
-    FrameShared* fs;                // the frame's claim queue and resolve plan
 };
 
 // wave-aggregated queue append: one atomic per wavefront
@@ -1430,6 +1389,12 @@ RT_D void block_tally(const bool (&pred)[K], uint32_t* const (&ctr)[K], uint32_t
     }
 }
 
+// Samples still to be claimed now: up to the partition's end, and (streaming splat) no further than
+// the record ring holds.
+RT_D unsigned long long remaining_samples(const Counters* c) {
+    const unsigned long long lim = c->claim_limit < c->total_samples ? c->claim_limit : c->total_samples;
+    return lim > c->next_sample ? lim - c->next_sample : 0ull;
+}
 
 // ---- lens (RT/raytracer.cpp:86-123)
 RT_D V2 transform_bokeh_sample(V2 o, float f, float n, float phi_shutter_max) {
@@ -1605,16 +1570,13 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_
     uint32_t before = 0;
     for (uint32_t w = 0; w < wave; ++w) before += pool.free_w[wbase - wave + w];
     const bool want = lane >= first;
-    const uint32_t blk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot / BLOCK));
-    const uint32_t g0 = blk & ~(CLAIM_GROUP - 1u);
-    const uint32_t cbase = pool.claim_base[blk / CLAIM_GROUP] +
-                           __ockl_wfred_add_u32(g0 + lane < blk ? pool.free_n[g0 + lane] : 0u);
-    const uint32_t remaining = cnt->claim_n;          // reserved by the last bookkeep (FrameShared)
+    const uint32_t cbase = pool.claim_base[slot / BLOCK];
+    const unsigned long long remaining = remaining_samples(cnt);
     const uint32_t claim = cbase + before + (lane - first);
     // No sample left for this block to claim (the frame's drain): its free slots go idle
-    const bool none_left = cbase >= remaining;
-    const bool active = !none_left && want && claim < remaining;
-    const unsigned long long k = cnt->claim_start + claim;
+    const bool none_left = (unsigned long long)cbase >= remaining;
+    const bool active = !none_left && want && (unsigned long long)claim < remaining;
+    const unsigned long long k = cnt->next_sample + claim;
     uint32_t x = 0, y = 0, s = 0, p = 0;
     if (active) {
         if (fp.list_xy) {
@@ -2072,13 +2034,6 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         new_path_records(fp, st, d4, t4, L4);
         state0 = S_TRACE;
     }
-    // the lowest key (sample pass, or list index) among the paths processed here (alive or finished,
-    // not yet splatted): LDS minima where each path's key is at hand, one entry per lane (no two lanes
-    // of a wave on one address), the block's to its shard's Counters::low_live at the tail (a pass is
-    // complete once no path of it is in flight)
-    __shared__ uint4 blow[64 / 4];
-    if (threadIdx.x < 64 / 4) blow[threadIdx.x] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    if (!IN_LDS) __syncthreads();                       // (scene_in_lds<true> has a barrier)
     const DevScene sc = scene_in_lds<IN_LDS>(sc_g, lds_scene);
     const bool valid = slot < pool.n && state0 == S_TRACE;             // traced this iteration
     bool cont = false, done = false, shadow = false, cast_shadow = false, enq = false;
@@ -2139,7 +2094,6 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
             for (int32_t lv = 1; lv <= at; ++lv)
                 pool.nx.mstack[(size_t)lv*pool.n + nslot] = pool.mstack[(size_t)lv*pool.n + slot];
         }
-        atomicMin(reinterpret_cast<uint32_t*>(blow) + __lane_id(), meta.y);
         const unsigned long long fm = made_fin_mask | __ballot(done);
         if (done) {                                        // everything but total_color
             const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fm & ((1ull << __lane_id()) - 1ull));
@@ -2186,7 +2140,6 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     const uint32_t fidx = (slot & ~63u) + (uint32_t)__popcll(fmask & ((1ull << __lane_id()) - 1ull));
     if (made_fin) {                                 // L = 0 with the vignette in .w (k_generate)
         const uint4 fmeta = stash[threadIdx.x];
-        atomicMin(reinterpret_cast<uint32_t*>(blow) + __lane_id(), fmeta.y);
         stnt(&pool.fin_L[fidx], pool.L[slot]);
         stnt(&pool.fin_k[fidx], make_uint2(fmeta.y, fmeta.w));
         stnt(&pool.fin_px[fidx], fmeta.x);
@@ -2230,20 +2183,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         pool.sh_slot[spos] = slot;
         pool.sh_dst[slot] = cont ? nslot : (SH_FIN | fidx);
     }
-    if (threadIdx.x == 0) {
-        pool.free_n[blockIdx.x] = ttot[5];
-        // the claim group's sum: a no-return atomic after the tally, off the block's critical path
-        // (64 blocks add to one word; as a 6th returning atomic in block_tally it delayed every block)
-        if (ttot[5]) __hip_atomic_fetch_add(&pool.group_sum[blockIdx.x / CLAIM_GROUP], ttot[5], __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t bl = 0xFFFFFFFFu;                       // every lane's LDS minimum is in: the tally's barriers
-#pragma unroll
-        for (int i = 0; i < 64 / 4; ++i) {
-            const uint4 b = blow[i];
-            bl = min(bl, min(min(b.x, b.y), min(b.z, b.w)));
-        }
-        if (bl != 0xFFFFFFFFu) __hip_atomic_fetch_min(&cnt->low_live[shard][0], bl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (threadIdx.x == 0) pool.free_n[blockIdx.x] = ttot[5];
 }
 
 
@@ -2578,9 +2518,8 @@ __global__ void __launch_bounds__(RES_BX*RES_BY) k_resolve(FrameParams fp) {
 // filter (cache_size 0) adds (L, 1) to the pixel's own sum in sample order, which IS the
 // reference's order.
 //
-// The frame's passes are resolved into the caller's buffer in pass order, one launch at a time
-// (FrameShared::res_busy), whichever partition's stream launches it: the frame does not depend on
-// the partitions.
+// Partition k resolves its own pass range into its own buffer (the caller's for k = 0),
+// so partitions never write the same buffer; k_combine_partials adds them up at the end.
 // Each pass's records are loaded at the start of that pass (r03b): 90 VGPRs, and the blocks find
 // room beside the other partitions' kernels sooner than with the next pass loading into registers
 // while this one is summed (120 VGPRs; C3 +0.2 %, C4 +0.6 %), at the cost of the load latency
@@ -2594,7 +2533,7 @@ template <int KSMAX>
 __global__ void __launch_bounds__(TR_THREADS) k_resolve_tiles(FrameParams fp, Pool pool, const Counters* cnt,
                                                                const uint32_t* blocks, float4* dst) {
     const uint32_t s0 = cnt->res_from, s1 = cnt->res_to;
-    if (s0 >= s1) return;                              // uniform: nothing planned (res_busy not ours)
+    if (s0 >= s1) return;
     constexpr int NST = tr_stage_slots(KSMAX);
     extern __shared__ float4 tr_lds[];
     const int ks = fp.cache_size ? fp.kernel_size : 0;
@@ -2699,218 +2638,202 @@ __global__ void __launch_bounds__(TR_THREADS) k_resolve_tiles(FrameParams fp, Po
         for (int r = 0; r < TR_ROWS; ++r)
             if (Y0 + r < H) dst[(size_t)(Y0 + r)*W + X] = acc[r];
     }
-    // The last block to finish: passes below s1 are resolved, so the ring may take claims up to pass
-    // s1 + ring, and the next resolve may be planned (FrameShared).  Every block's stores are released
-    // (agent scope: the other XCDs' L2s) before it counts itself.
-    __syncthreads();
-    if (tid == 0) {
-        FrameShared* fs = fp.fs;
-        __threadfence();
-        if (atomicAdd(&fs->res_blocks, 1u) == gridDim.x - 1u) {
-            __threadfence();
-            fs->res_blocks = 0u;
-            atomicMax(&fs->claim_limit, (unsigned long long)(s1 + pool.rec_ring)*fp.pixels);
-            __hip_atomic_store(&fs->res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The partitions' buffers added to the caller's, in partition order (streaming splat).
+__global__ void __launch_bounds__(256) k_combine_partials(float4* accum, const float4* const* parts, int nparts, size_t n) {
+    for (size_t i = (size_t)blockIdx.x*256 + threadIdx.x; i < n; i += (size_t)gridDim.x*256) {
+        float4 a = accum[i];
+        for (int k = 0; k < nparts; ++k) {
+            const float4 b = ldnt(&parts[k][i]);
+            a.x = a.x + b.x; a.y = a.y + b.y; a.z = a.z + b.z; a.w = a.w + b.w;
         }
+        accum[i] = a;
     }
 }
 
-// k_bookkeep — end of iteration (one wave): ray counts, counter roll-over, the scan of the claim
-// groups' free counts that gives every block of the next k_generate its first claim, the
-// reservation of those claims from the frame's queue (FrameShared), and the resolve plan.  Phase
-// BK_FIRST = before the first iteration (the scan and the first reservation); BK_FINAL = after every
-// partition's last iteration, the streams joined (only the plan of the passes left).
+// k_bookkeep — end of iteration (one workgroup): ray counts, counter roll-over,
+// and the exclusive scan of the per-block free counts that gives every block of
+// the next k_generate its first sample claim.  Phase BK_FIRST = before the first
+// iteration (only the scan); BK_FINAL = after the partition's last iteration (only
+// the resolve plan).
 //
-// Streaming splat: a path claimed by the k_generate of iteration j has made its last bounce by the
-// k_shade of iteration j + max(max_bounce_count, 1) - 1 (one bounce per iteration), and its sample
-// record is written by the next k_generate.  So once iteration i is bookkept, every sample the
-// partition claimed up to iteration i - life is in the record ring (life = max(max_bounce_count, 1)):
-// its claims younger than that (hist_a / hist_n) are what it may still have in flight (FrameShared::
-// low).  With plan.mode set (the host launches k_resolve_tiles right after this kernel), and no other
-// resolve planned and unfinished, the passes complete since the last plan become the next resolve's
-// range once there are plan.chunk of them (or all that remain); the resolve's last block moves the
-// claim limit so that the ring never overwrites a pass not yet resolved.
+// Streaming splat: a path claimed by the k_generate of iteration j has made its last
+// bounce by the k_shade of iteration j + max(max_bounce_count, 1) - 1 (one bounce per
+// iteration), and its sample record is written by the next k_generate.  So once
+// iteration i is bookkept, every sample claimed up to iteration i - life is in the
+// record ring (life = max(max_bounce_count, 1)): hist[] holds the claim cursor per
+// iteration.  With plan.mode set (the host launches k_resolve_tiles right after this
+// kernel), the passes complete since the last plan become the next resolve's range
+// once there are plan.chunk of them (or all that remain, BK_FINAL), and the claim
+// limit moves to keep the ring from overwriting passes not yet resolved.
 enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
 // fuse: set Counters::fused once nothing is left to claim and at most this many paths are alive
 // (0: never; see k_drain)
 // cast0: max_bounce_count > 0, so every sample claimed this iteration casts a camera ray (k_bookkeep counts
 // them from the claims; k_generate keeps no counter for them)
-// part, nparts: this partition and the frame's partition count (FrameShared::low)
-// listed: an explicit sample list (rt_trace_samples): a path's key is its sample number
-struct ResPlan { uint32_t mode, P, pass1, chunk, life, fuse, cast0, part, nparts, listed; };
-// One wave (r05).  It used to scan every block's free count itself (up to 32k, one workgroup of 512 or
-// 1024 threads): 32 us alone but 342 us beside the other partitions' kernels, a workgroup of 8-16 waves
-// waiting for room on one CU (9.5 % of C3's kernel time, profiles/r04_c3_pmc.md).  Now k_shade adds its
-// free count to its claim group's sum and this wave scans the group sums only (Pool::group_sum).
-constexpr int BK_THREADS = 64;
-constexpr unsigned long long NO_SAMPLE = ~0ull;
-RT_D unsigned long long ld_acq(const unsigned long long* p) { return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT); }
-RT_D void st_rel(unsigned long long* p, unsigned long long v) { __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT); }
-__global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, FrameShared* fs, Pool pool, uint32_t nblocks,
-                                                         int cur, int phase, ResPlan plan) {
+struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0; };
+// Two workgroup sizes, picked per frame by the partition's pool (BK_LARGE_POOL): a pool of 4M paths or
+// more (a whole 1080p frame: 8.4M) takes the 512-thread build (92 VGPRs: 8 waves that find room beside
+// the other partitions' kernels sooner), a smaller one (a rank's share of a multi-GPU frame: 3.3M) the
+// 1024-thread build (62 VGPRs, 16 waves on one CU).  A/B (profiles/r03b_ab.txt section 14): 256 threads
+// (156 VGPRs) gave the full C3 frame +0.5 to +0.9 % and C4 +1.2 to +1.5 % over 1024, but rank 0 of 8
+// -1.9 to -2.8 %; with the 96-VGPR trace kernels 512 threads give C3 +1.5 to +2.2 % over 256 and C4 -0.1 to
+// -1.0 % (profiles/r04_bookkeep_ab.txt).
+constexpr int BK_THREADS_SMALL = 1024, BK_THREADS_LARGE = 512;
+constexpr uint32_t BK_LARGE_POOL = 4u << 20;
+template <int BK_THREADS>
+__global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
+                                                         ResPlan plan) {
+    __shared__ uint32_t sc[BK_THREADS];
+    __shared__ uint32_t carry;
     const uint32_t t = threadIdx.x;
-    if (phase == BK_FINAL) {                   // every stream joined: no resolve is running
+    if (phase == BK_FINAL) {
         if (t == 0) {
-            const uint32_t from = fs->res_cursor;
-            const bool any = from < plan.pass1;
-            cnt->res_from = any ? from : 0u;
-            cnt->res_to = any ? plan.pass1 : 0u;
-            if (any) { fs->res_cursor = plan.pass1; fs->res_busy = 1u; }
+            cnt->res_from = cnt->res_cursor;
+            cnt->res_to = plan.pass1;
+            cnt->res_cursor = plan.pass1;
         }
         return;
     }
-    // The group sums' loads go out first, so they overlap the counter work below: lane t owns the
-    // contiguous groups [t*E, t*E + E), up to BK_EMAX of them in registers (pools up to 32M paths).
-    constexpr uint32_t BK_EMAX = 32;
-    const uint32_t ngroups = (nblocks + CLAIM_GROUP - 1) / CLAIM_GROUP;
-    const uint32_t E = (ngroups + BK_THREADS - 1) / BK_THREADS;
-    const uint32_t lo = t*E, hi = min(lo + E, ngroups);
+    // The free counts' loads go out first, so they overlap the counter work below.
+    // Up to BK_EMAX entries per thread (pools up to 32k blocks, 8.4M paths) are loaded at once into
+    // registers, all in flight, and the claims are written from them; a loop covers larger pools.
+    constexpr uint32_t BK_EMAX = 32*(1024 / BK_THREADS);
+    const uint32_t E = (nblocks + BK_THREADS - 1) / BK_THREADS;
+    const uint32_t lo = t*E, hi = min(lo + E, nblocks);
     uint32_t v[BK_EMAX];
     if (E <= BK_EMAX) {
 #pragma unroll
-        for (uint32_t j = 0; j < BK_EMAX; ++j) {
-            const uint32_t g = lo + j;
-            // before the first iteration every block is free (free_n = BLOCK, set by the host)
-            v[j] = g >= hi ? 0u : phase == BK_FIRST ? (min(nblocks - g*CLAIM_GROUP, CLAIM_GROUP)*BLOCK)
-                                                    : pool.group_sum[g];
+        for (uint32_t j = 0; j < BK_EMAX; ++j) v[j] = lo + j < hi ? pool.free_n[lo + j] : 0u;
+    }
+    __shared__ uint32_t skip;
+    if (t < 64) {
+        // Lane k < NSHARD reads shard k's counters, all loads in flight, and the sums come from
+        // shuffles.  (Thread 0 alone walking the shards, each load ordered behind the previous
+        // shard's stores, took ~60 dependent round trips: 27 us alone, ~290 us beside the other
+        // partitions' kernels, 10 % of a partition's iteration.)
+        const bool it_phase = phase == BK_ITER;
+        const uint32_t done_flag = it_phase ? cnt->done : 0u;
+        uint32_t al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
+        if (it_phase && t < NSHARD) {
+            al = cnt->alive[t][0];
+            c1 = cnt->cast[1][t][0];
+            us = cnt->unsplat[t][0];
+            eq = cnt->ext_count[cur][t][0];
+            sq = cnt->shadow_count[t][0];
+        }
+        unsigned long long next = 0, total = 0, lim = 0, start = 0;
+        uint32_t gfree = 0, it = 0, rcur = 0;
+        if (t == 0 && it_phase) {
+            next = cnt->next_sample; total = cnt->total_samples; lim = cnt->claim_limit;
+            start = cnt->start_sample; gfree = cnt->gen_free; it = cnt->iter; rcur = cnt->res_cursor;
+        }
+        // the claim cursor `life` iterations ago (loaded before any store to the counters)
+        const unsigned long long done_cursor =
+            (t == 0 && it_phase && plan.mode && it >= plan.life) ? cnt->hist[(it - plan.life) & 127u] : start;
+        const bool sk = it_phase && done_flag;
+        if (it_phase && !sk && t < NSHARD) {
+            cnt->unsplat[t][0] = 0;
+            cnt->cast[1][t][0] = 0;
+            cnt->alive[t][0] = 0;
+            cnt->ext_count[cur][t][0] = 0;
+            cnt->shadow_count[t][0] = 0;
+            cnt->fetch[0][t][0] = 0;
+            cnt->fetch[1][t][0] = 0;
+        }
+        uint32_t ext = al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
+#pragma unroll
+        for (int off = 1; off < NSHARD; off <<= 1) {
+            ext += __shfl_xor(ext, off); sh += __shfl_xor(sh, off); pend += __shfl_xor(pend, off);
+            ps += __shfl_xor(ps, off); tq += __shfl_xor(tq, off); ts += __shfl_xor(ts, off);
+        }
+        if (t == 0) {
+            skip = sk;
+            if (sk) {
+                // done: the passes the bookkeep that found it complete could not plan (an iteration
+                // without a resolve after it) are resolved after this one, on the device, instead of
+                // waiting for the host's BK_FINAL
+                const bool last = plan.mode && rcur < plan.pass1;
+                cnt->res_from = last ? rcur : 0u;
+                cnt->res_to = last ? plan.pass1 : 0u;
+                if (last) cnt->res_cursor = plan.pass1;
+            }
+            if (it_phase && !sk) {
+                const unsigned long long lm = lim < total ? lim : total;
+                const unsigned long long rem = lm > next ? lm - next : 0ull;      // remaining_samples()
+                const unsigned long long claimed = (unsigned long long)gfree < rem ? (unsigned long long)gfree : rem;
+                next += claimed;
+                cnt->next_sample = next;
+                // the camera rays of this iteration's k_generate: one per claimed sample (every claim below
+                // the remaining count becomes a path, k_generate) when max_bounce_count > 0
+                cnt->closest_rays += ext + (plan.cast0 ? claimed : 0ull);
+                cnt->shadow_rays += sh;
+                cnt->traced_rays[0] += tq;
+                cnt->traced_rays[1] += ts;
+                cnt->pending = pend;
+                cnt->pending_splat = ps;
+                // nothing left to claim, trace or splat: every record is in the ring
+                const bool complete = next >= total && pend == 0 && ps == 0;
+                if (complete) cnt->done = 1;
+                else if (plan.fuse && next >= total && pend <= plan.fuse) cnt->fused = 1;
+                cnt->iter = it + 1;
+                cnt->hist[it & 127u] = next;
+                if (plan.mode) {
+                    const uint32_t done_pass = complete ? plan.pass1 : (uint32_t)(done_cursor / plan.P);
+                    const uint32_t from = rcur;
+                    cnt->res_from = cnt->res_to = 0;
+                    if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
+                        cnt->res_from = from;
+                        cnt->res_to = done_pass;
+                        cnt->res_cursor = done_pass;
+                        // the ring slots of [from, done_pass) are free once the resolve launched next has run
+                        cnt->claim_limit = (unsigned long long)(done_pass + plan.ring)*plan.P;
+                    }
+                }
+            }
+            carry = 0;
         }
     }
-    // Lane k < NSHARD reads shard k's counters, all loads in flight, and the sums come from
-    // shuffles.  (Thread 0 alone walking the shards, each load ordered behind the previous
-    // shard's stores, took ~60 dependent round trips: 27 us alone, ~290 us beside the other
-    // partitions' kernels, 10 % of a partition's iteration.)
-    const bool it_phase = phase == BK_ITER;
-    const uint32_t done_flag = it_phase ? cnt->done : 0u;
-    if (done_flag) {                                   // uniform: the partition is complete
-        if (t == 0 && plan.mode) cnt->res_from = cnt->res_to = 0;   // the resolve launched next: nothing
-        return;
-    }
-    const uint32_t it = cnt->iter;                     // iterations bookkept so far
-    uint32_t al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
-    if (it_phase && t < NSHARD) {
-        al = cnt->alive[t][0];
-        c1 = cnt->cast[1][t][0];
-        us = cnt->unsplat[t][0];
-        eq = cnt->ext_count[cur][t][0];
-        sq = cnt->shadow_count[t][0];
-    }
-    // this partition's lowest sample still in flight: the paths its k_shade processed this iteration
-    // (alive, or finished and splatted by the next k_generate); the claims of the k_generate that ran
-    // were among them
-    unsigned long long low_prev = NO_SAMPLE;
-    {
-        uint32_t l = (it_phase && t < NSHARD) ? cnt->low_live[t][0] : 0xFFFFFFFFu;
-#pragma unroll
-        for (int off = 1; off < NSHARD; off <<= 1) l = min(l, (uint32_t)__shfl_xor(l, off));
-        if (l != 0xFFFFFFFFu) low_prev = plan.listed ? (unsigned long long)l : (unsigned long long)l*plan.P;
-    }
-    if (it_phase && t < NSHARD) {
-        cnt->low_live[t][0] = 0xFFFFFFFFu;
-        cnt->unsplat[t][0] = 0;
-        cnt->cast[1][t][0] = 0;
-        cnt->alive[t][0] = 0;
-        cnt->ext_count[cur][t][0] = 0;
-        cnt->shadow_count[t][0] = 0;
-        cnt->fetch[0][t][0] = 0;
-        cnt->fetch[1][t][0] = 0;
-    }
-    uint32_t ext = al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
-#pragma unroll
-    for (int off = 1; off < NSHARD; off <<= 1) {
-        ext += __shfl_xor(ext, off); sh += __shfl_xor(sh, off); pend += __shfl_xor(pend, off);
-        ps += __shfl_xor(ps, off); tq += __shfl_xor(tq, off); ts += __shfl_xor(ts, off);
-    }
-    // exclusive scan of the group sums: lane t sums its groups, a wave scan by shuffles; the group
-    // sums are zeroed for the next k_shade (which runs after the k_generate that reads claim_base)
+    __syncthreads();
+    if (skip) return;
+    // exclusive scan of free_n: thread t owns the contiguous entries [t*E, t*E + E), sums them,
+    // then a wave scan by shuffles and one barrier for the 16 wave totals.
+    // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
+    // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
     uint32_t sum = 0;
     if (E <= BK_EMAX) {
 #pragma unroll
         for (uint32_t j = 0; j < BK_EMAX; ++j) sum += v[j];
     } else {
-        for (uint32_t g = lo; g < hi; ++g)
-            sum += phase == BK_FIRST ? min(nblocks - g*CLAIM_GROUP, CLAIM_GROUP)*BLOCK : pool.group_sum[g];
+        for (uint32_t i = lo; i < hi; ++i) sum += pool.free_n[i];
     }
+    const uint32_t lane = t & 63u, wave = t >> 6;
     uint32_t incl = sum;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const uint32_t u = __shfl_up(incl, off);
-        if (t >= (uint32_t)off) incl += u;
+        if (lane >= (uint32_t)off) incl += u;
     }
-    uint32_t run = incl - sum;
+    if (lane == 63) sc[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += sc[w];
+    uint32_t run = before + incl - sum;
     if (E <= BK_EMAX) {
 #pragma unroll
         for (uint32_t j = 0; j < BK_EMAX; ++j)
-            if (lo + j < hi) { pool.claim_base[lo + j] = run; pool.group_sum[lo + j] = 0u; run += v[j]; }
+            if (lo + j < hi) { pool.claim_base[lo + j] = run; run += v[j]; }
     } else {
-        for (uint32_t g = lo; g < hi; ++g) {
-            const uint32_t x = phase == BK_FIRST ? min(nblocks - g*CLAIM_GROUP, CLAIM_GROUP)*BLOCK : pool.group_sum[g];
-            pool.claim_base[g] = run;
-            pool.group_sum[g] = 0u;
+        for (uint32_t i = lo; i < hi; ++i) {
+            const uint32_t x = pool.free_n[i];
+            pool.claim_base[i] = run;
             run += x;
         }
     }
-    const uint32_t gen_free = __shfl(incl, 63);        // the next k_generate's free slots
-    if (t == 0) {
-        // the claims the k_generate that just ran took (reserved by the last bookkeep)
-        const uint32_t claimed = it_phase ? cnt->claim_n : 0u;
-        if (it_phase) {
-            cnt->closest_rays += ext + (plan.cast0 ? (unsigned long long)claimed : 0ull);
-            cnt->shadow_rays += sh;
-            cnt->traced_rays[0] += tq;
-            cnt->traced_rays[1] += ts;
-            cnt->pending = pend;
-            cnt->pending_splat = ps;
-        }
-        // nothing of this partition alive or waiting for its splat: no claim of it is in flight
-        if (it_phase && pend == 0 && ps == 0) low_prev = NO_SAMPLE;
-        // Reserve the next k_generate's claims.  A lower bound of them is published as this
-        // partition's low first, so a planner that sees the moved cursor also sees it.
-        unsigned long long nx = ld_acq(&fs->next_sample);
-        st_rel(&fs->low[plan.part], min(low_prev, nx));
-        const unsigned long long total = fs->total_samples;
-        const unsigned long long lim0 = ld_acq(&fs->claim_limit);
-        const unsigned long long lim = lim0 < total ? lim0 : total;
-        unsigned long long a = nx;
-        uint32_t n = 0;
-        for (;;) {
-            a = nx;
-            n = lim > a ? (uint32_t)min(lim - a, (unsigned long long)gen_free) : 0u;
-            if (n == 0) break;
-            const unsigned long long seen = atomicCAS(&fs->next_sample, a, a + n);
-            if (seen == a) { nx = a + n; break; }
-            nx = seen;
-        }
-        cnt->claim_start = a;
-        cnt->claim_n = n;
-        st_rel(&fs->low[plan.part], n ? min(low_prev, a) : low_prev);
-        cnt->next_sample = nx;
-        cnt->total_samples = total;
-        if (it_phase) {
-            // nothing left to claim, trace or splat: every record of this partition is in the ring
-            const bool complete = nx >= total && pend == 0 && ps == 0 && n == 0;
-            if (complete) cnt->done = 1;
-            else if (plan.fuse && nx >= total && pend <= plan.fuse) cnt->fused = 1;
-            cnt->iter = it + 1;
-        }
-        if (plan.mode) cnt->res_from = cnt->res_to = 0;
-        // the planner: no other resolve planned and unfinished (its last block clears res_busy)
-        if (plan.mode && atomicCAS(&fs->res_busy, 0u, 1u) == 0u) {
-            __threadfence();                                   // acquire: the last resolve's cursor and limit
-            // every sample below min(cursor, lows) is splatted: the passes below it are complete
-            unsigned long long m = ld_acq(&fs->next_sample);
-            for (uint32_t k = 0; k < plan.nparts; ++k) m = min(m, ld_acq(&fs->low[k]));
-            m = min(m, total);
-            const uint32_t done_pass = (uint32_t)min(m / plan.P, (unsigned long long)plan.pass1);
-            const uint32_t from = __hip_atomic_load(&fs->res_cursor, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (done_pass > from && (done_pass - from >= plan.chunk || done_pass >= plan.pass1)) {
-                cnt->res_from = from;
-                cnt->res_to = done_pass;
-                fs->res_cursor = done_pass;                // res_busy stays set until the resolve's last block
-            } else {
-                __hip_atomic_store(&fs->res_busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
+    if (t == BK_THREADS - 1) carry = run;
+    __syncthreads();
+    if (t == 0) cnt->gen_free = carry;
 }
 
 // debug / parity kernel: intersect_scene / intersect_shadow_ray for explicit rays,
@@ -3060,9 +2983,9 @@ struct rt_scene {
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
     float* d_lut = nullptr;
-    FrameShared* d_fs = nullptr;    // the frame's claim queue and resolve plan
-    FrameShared* h_fs = nullptr;    // pinned: the frame's initial FrameShared
-    uint32_t* d_aux = nullptr;      // streaming splat: k_resolve_tiles' blocks
+    float4* d_partials = nullptr;   // streaming splat: partitions 1.. accumulate here
+    size_t partial_cap = 0;
+    uint32_t* d_aux = nullptr;      // streaming splat: partial pointers, then k_resolve_tiles' blocks
     size_t aux_cap = 0;
     // The frame layout of the last rt_render_device (owned tiles, pixel map, tile bases, resolve
     // blocks): rebuilt and uploaded only when the frame size, tiling, shard or filter radius changes.
@@ -3074,6 +2997,9 @@ struct rt_scene {
         std::vector<int32_t> base;
         int blocks_ks = -1;                 // radius the resolve blocks were built for (-1: none)
         uint32_t nblocks = 0;
+        const void* aux_partials = nullptr; // d_partials / npx the device pointer table holds
+        size_t aux_npx = 0;
+        int aux_parts = -1;
     } layout;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
@@ -3266,9 +3192,7 @@ int ensure_pool(Partition& pt, uint32_t n) {
     const size_t Q = cap*NSHARD;
     p.shard_cap = (uint32_t)cap;
     e |= alloc((void**)&p.free_n, 4*nblocks);
-    const size_t ngroups = (nblocks + CLAIM_GROUP - 1) / CLAIM_GROUP;
-    e |= alloc((void**)&p.claim_base, 4*ngroups);
-    e |= alloc((void**)&p.group_sum, 4*ngroups);
+    e |= alloc((void**)&p.claim_base, 4*nblocks);
     e |= alloc((void**)&p.fin_w, 4*(N / 64));
     e |= alloc((void**)&p.free_w, 4*(N / 64));
     e |= alloc((void**)&p.fin_L, 16*N);
@@ -3365,13 +3289,15 @@ struct SplatCfg {
     int mode = RT_SPLAT_ATOMIC;         // rt_splat_mode; ATOMIC also for explicit sample lists
     uint32_t passes = 0;                // the frame's sample passes (of this shard)
     uint32_t pass_lo = 0;               // its first pass (RT_SHARD_PASSES: the shard's range)
-    uint32_t ring = 0, chunk = 0;       // STREAM: record-ring passes, passes per resolve
-    float4* rec = nullptr;              // STREAM: a ring of ring*P; EXACT: spp*P, pass-major
+    uint32_t ring = 0, chunk = 0;       // STREAM: record-ring passes per partition, passes per resolve
+    float4* rec = nullptr;              // STREAM: nparts rings of ring*P; EXACT: spp*P, pass-major
     float* rec_jy = nullptr;
     const uint32_t* blocks = nullptr;   // STREAM: k_resolve_tiles' output blocks
     uint32_t nblocks = 0;
     int ksmax = 2;                      // STREAM: k_resolve_tiles instantiation
     size_t lds = 0;
+    float4* partials = nullptr;         // STREAM: partitions 1.. accumulate here (w*h each)
+    const float4* const* part_ptrs = nullptr;   // device array of the partials' addresses
 };
 
 void launch_resolve_tiles(const SplatCfg& sp, const FrameParams& fp, const Pool& pool, const Counters* cnt,
@@ -3396,39 +3322,25 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
               const SplatCfg& sp, rt_stats* stats) {
     auto t0 = std::chrono::steady_clock::now();
     const bool listed = fp.list_xy != nullptr;
-    fp.fs = s->d_fs;
     const FrameShape shape = frame_shape(s, total, listed ? 0u : sp.passes);
     const int nparts = shape.nparts;
     const uint32_t pool_n = shape.pool_n;
-    FrameShared* const fs = s->d_fs;
-    auto launch_bookkeep = [fs](Counters* c, const Pool& pl, uint32_t nblocks, int cur, int phase, ResPlan plan,
-                                hipStream_t q) {
-        k_bookkeep<<<1, BK_THREADS, 0, q>>>(c, fs, pl, nblocks, cur, phase, plan);
+    // k_bookkeep's workgroup size by the pool (BK_LARGE_POOL, see k_bookkeep)
+    const bool bk_large = pool_n >= BK_LARGE_POOL;
+    auto launch_bookkeep = [bk_large](Counters* c, const Pool& pl, uint32_t nblocks, int cur, int phase, ResPlan plan,
+                                      hipStream_t q) {
+        if (bk_large) k_bookkeep<BK_THREADS_LARGE><<<1, BK_THREADS_LARGE, 0, q>>>(c, pl, nblocks, cur, phase, plan);
+        else k_bookkeep<BK_THREADS_SMALL><<<1, BK_THREADS_SMALL, 0, q>>>(c, pl, nblocks, cur, phase, plan);
     };
     const bool stream_splat = !listed && sp.mode == RT_SPLAT_STREAM;
+    const size_t npx = (size_t)fp.w*fp.h;
     const uint32_t prof = g_profiling & ~(1u << RT_KERNEL_SPLAT);   // the splat runs inside k_generate
     const int diag = s->cfg.debug_traversal ? 1 : 0;
     if (!s->start_ev) HIP_OK(hipEventCreateWithFlags(&s->start_ev, hipEventDisableTiming));
-    // The frame's queue: samples [start, end) (absolute: pass * P + pixel, or list indices), the ring's
-    // first claim limit, no partition holding anything, no resolve planned.
-    const unsigned long long q_start = listed ? 0ull : (unsigned long long)sp.pass_lo*fp.pixels;
-    const unsigned long long q_end = listed ? total : (unsigned long long)(sp.pass_lo + sp.passes)*fp.pixels;
-    {
-        FrameShared& h = *s->h_fs;
-        memset(&h, 0, sizeof(h));
-        h.next_sample = q_start;
-        h.total_samples = q_end;
-        h.claim_limit = stream_splat ? (unsigned long long)(sp.pass_lo + sp.ring)*fp.pixels : ~0ull;
-        for (auto& l : h.low) l = ~0ull;
-        h.res_cursor = sp.pass_lo;
-        h.ring = sp.ring;
-        // pinned: the copy is asynchronous (the previous frame has ended, the next one waits for this one)
-        HIP_OK(hipMemcpyAsync(s->d_fs, s->h_fs, sizeof(FrameShared), hipMemcpyHostToDevice, stream));
-    }
     HIP_OK(hipEventRecord(s->start_ev, stream));
     struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live, drain, near;
                  unsigned long long seen_next; int final_buf;
-                 uint64_t chunk_first[2]; int chunk_n[2];
+                 uint64_t chunk_first[2]; int chunk_n[2]; uint32_t pass0, pass1, ring; float4* dst;
                  bool res_ev[EV_SLOTS]; };
     Run run[MAX_PARTITIONS] = {};
     double kms[RT_KERNEL_COUNT] = {};
@@ -3441,10 +3353,6 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     const uint32_t fuse_paths = s->cfg.fuse_paths >= 0
         ? (uint32_t)std::min<int64_t>(s->cfg.fuse_paths, 0xFFFFFFFFll)
         : std::max(s->drain_lanes_full*5u/2u, pool_n / 10u);
-    auto plan_of = [&](int k, uint32_t mode) {
-        return ResPlan{mode, fp.pixels, sp.pass_lo + sp.passes, sp.chunk, life, fuse_paths,
-                       st->max_bounce_count > 0 ? 1u : 0u, (uint32_t)k, (uint32_t)nparts, listed ? 1u : 0u};
-    };
     for (int k = 0; k < nparts; ++k) {
         int err = ensure_partition(s, k);
         if (!err) err = ensure_pool(s->part[k], pool_n);
@@ -3457,36 +3365,52 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         r.grid = (N + BLOCK - 1) / BLOCK;
         r.live = true;
         Counters init = {};
-        for (auto& l : init.low_live) l[0] = 0xFFFFFFFFu;
-        init.next_sample = q_start;
-        init.total_samples = q_end;
+        init.claim_limit = ~0ull;
         Pool& pool = pt.pool;
-        // every partition's sample records go to the frame's one record array (FrameShared)
-        pool.rec_rgbx = nullptr; pool.rec_jy = nullptr; pool.rec_pass0 = sp.pass_lo; pool.rec_ring = 1;
-        if (!listed && sp.mode == RT_SPLAT_EXACT) {             // the global pass-major layout, s*P + p
-            pool.rec_rgbx = sp.rec + (size_t)sp.pass_lo*fp.pixels;
-            pool.rec_jy = sp.rec_jy + (size_t)sp.pass_lo*fp.pixels;
-            pool.rec_ring = std::max(1u, sp.passes);
-        } else if (stream_splat) {                               // a ring of sp.ring passes
-            pool.rec_rgbx = sp.rec;
-            pool.rec_jy = sp.rec_jy;
-            pool.rec_ring = sp.ring;
+        pool.rec_rgbx = nullptr; pool.rec_jy = nullptr; pool.rec_pass0 = 0; pool.rec_ring = 1;
+        if (listed) {
+            init.next_sample = total*(unsigned long long)k / nparts;
+            init.total_samples = total*(unsigned long long)(k + 1) / nparts;
+        } else {
+            r.pass0 = sp.pass_lo + (uint32_t)((unsigned long long)sp.passes*k / nparts);
+            r.pass1 = sp.pass_lo + (uint32_t)((unsigned long long)sp.passes*(k + 1) / nparts);
+            init.next_sample = (unsigned long long)r.pass0*fp.pixels;
+            init.total_samples = (unsigned long long)r.pass1*fp.pixels;
+            init.res_cursor = r.pass0;
+            pool.rec_pass0 = r.pass0;
+            if (sp.mode == RT_SPLAT_EXACT) {                   // the global pass-major layout, s*P + p
+                pool.rec_rgbx = sp.rec + (size_t)r.pass0*fp.pixels;
+                pool.rec_jy = sp.rec_jy + (size_t)r.pass0*fp.pixels;
+                pool.rec_ring = std::max(1u, r.pass1 - r.pass0);
+            } else if (stream_splat) {
+                r.ring = std::min(sp.ring, std::max(1u, r.pass1 - r.pass0));
+                pool.rec_rgbx = sp.rec + (size_t)k*sp.ring*fp.pixels;
+                pool.rec_jy = sp.rec_jy + (size_t)k*sp.ring*fp.pixels;
+                pool.rec_ring = r.ring;
+                init.claim_limit = (unsigned long long)(r.pass0 + r.ring)*fp.pixels;
+                r.dst = k ? sp.partials + (size_t)(k - 1)*npx : fp.accum;
+                if (k) HIP_OK(hipMemsetAsync(r.dst, 0, sizeof(float4)*npx, r.stream));
+            }
         }
+        init.start_sample = init.next_sample;
         r.seen_next = init.next_sample;
         pt.cnt_host[2] = init;           // pinned: the copy is asynchronous (the frame ends before the next write)
         HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + 2, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
-        // (the group sums are zeroed by the BK_FIRST bookkeep below, which scans the all-free pool)
         HIP_OK(hipMemsetAsync(pt.pool.fin_w, 0, 4ull*N / 64, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_w, 64, N / 64, r.stream));
-        launch_bookkeep(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, plan_of(k, 0u), r.stream);
+        launch_bookkeep(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{}, r.stream);
         if (prof && !pt.events) {
             for (auto& e : pt.ev) HIP_OK(hipEventCreate(&e));
             for (auto& e : pt.ev_final) HIP_OK(hipEventCreate(&e));
             pt.events = true;
         }
     }
+    auto plan_of = [&](int k, uint32_t mode) {
+        const Run& r = run[k];
+        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, life, fuse_paths, st->max_bounce_count > 0 ? 1u : 0u};
+    };
     // Stage timing without extra host syncs: each iteration records begin/end
     // events into one of EV_SLOTS ring slots; a chunk's slots are read back when
     // the host has waited for that chunk anyway.
@@ -3559,7 +3483,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         r.res_ev[slot] = res && ((prof >> RT_KERNEL_RESOLVE) & 1u);
         if (res) {                       // the passes the bookkeep found complete, if enough of them
             b(RT_KERNEL_RESOLVE);
-            launch_resolve_tiles(sp, fp, pv, pt.cnt, fp.accum, q);
+            launch_resolve_tiles(sp, fp, pv, pt.cnt, r.dst, q);
             e(RT_KERNEL_RESOLVE);
         }
         ++r.iters;
@@ -3580,6 +3504,19 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         HIP_OK(hipMemcpyAsync(pt.cnt_host + b, pt.cnt, sizeof(Counters), hipMemcpyDeviceToHost, r.stream));
         HIP_OK(hipEventRecord(pt.chunk_done[b], r.stream));
         ++r.chunks;
+        return RT_OK;
+    };
+    // A partition whose samples are all splatted resolves whatever passes are left.
+    auto finish = [&](int k) -> int {
+        if (!stream_splat) return RT_OK;
+        Partition& pt = s->part[k];
+        Run& r = run[k];
+        launch_bookkeep(pt.cnt, pt.pool, r.grid, r.cur, BK_FINAL, plan_of(k, 2u), r.stream);
+        const bool t = (prof >> RT_KERNEL_RESOLVE) & 1u;
+        if (t) HIP_OK(hipEventRecord(pt.ev_final[0], r.stream));
+        launch_resolve_tiles(sp, fp, pt.pool, pt.cnt, r.dst, r.stream);
+        if (t) HIP_OK(hipEventRecord(pt.ev_final[1], r.stream));
+        HIP_OK(hipGetLastError());
         return RT_OK;
     };
     s->cancel = 0;
@@ -3607,9 +3544,10 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             // fused-drain kernels (two chunks are in flight when the host sees a chunk's counters)
             if (c.next_sample + 2*(c.next_sample - r.seen_next) >= c.total_samples) r.near = true;
             r.seen_next = c.next_sample;
-            // the queue is empty and nothing of the partition is alive, unsplatted or reserved
-            if (c.next_sample >= c.total_samples && c.pending == 0 && c.pending_splat == 0 && c.claim_n == 0) {
+            if (c.next_sample >= c.total_samples && c.pending == 0 && c.pending_splat == 0) {
                 r.live = false; r.final_buf = b; --live;       // its chunk still in flight finds nothing to do
+                int err = finish(k);
+                if (err) return err;
             } else {
                 int err = enqueue_chunk(k);
                 if (err) return err;
@@ -3629,19 +3567,16 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         HIP_OK(hipEventRecord(s->part[k].join, run[k].stream));
         HIP_OK(hipStreamWaitEvent(stream, s->part[k].join, 0));
     }
-    // every stream joined: the passes no planner resolved (the last ones) on the caller's stream
-    if (stream_splat) {
-        Partition& pt = s->part[0];
-        const bool t = (prof >> RT_KERNEL_RESOLVE) & 1u;
-        launch_bookkeep(pt.cnt, pt.pool, run[0].grid, run[0].cur, BK_FINAL, plan_of(0, 2u), stream);
-        if (t) HIP_OK(hipEventRecord(pt.ev_final[0], stream));
-        launch_resolve_tiles(sp, fp, pt.pool, pt.cnt, fp.accum, stream);
-        if (t) HIP_OK(hipEventRecord(pt.ev_final[1], stream));
+    if (stream_splat && nparts > 1) {
+        k_combine_partials<<<(uint32_t)std::min<size_t>((npx + 255) / 256, 8192), 256, 0, stream>>>(
+            fp.accum, sp.part_ptrs, nparts - 1, npx);
         HIP_OK(hipGetLastError());
-        if (t) {
-            HIP_OK(hipStreamSynchronize(stream));
+    }
+    if (stream_splat && ((prof >> RT_KERNEL_RESOLVE) & 1u)) {
+        HIP_OK(hipStreamSynchronize(stream));
+        for (int k = 0; k < nparts; ++k) {
             float ms = 0.0f;
-            if (hipEventElapsedTime(&ms, pt.ev_final[0], pt.ev_final[1]) == hipSuccess) {
+            if (hipEventElapsedTime(&ms, s->part[k].ev_final[0], s->part[k].ev_final[1]) == hipSuccess) {
                 kms[RT_KERNEL_RESOLVE] += ms; klaunch[RT_KERNEL_RESOLVE] += 1;
             }
         }
@@ -4194,8 +4129,6 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         s->drain_grid = std::max(1u, (uint32_t)((unsigned long long)s->drain_grid*(unsigned long long)drain_pct / 100ull));
     }
     if (ensure_partition(s, 0)) return fail(RT_ERROR_OUT_OF_MEMORY);
-    if (hipMalloc(&s->d_fs, sizeof(FrameShared)) != hipSuccess ||
-        hipHostMalloc(&s->h_fs, sizeof(FrameShared)) != hipSuccess) { set_error("hipMalloc frame state"); return fail(RT_ERROR_OUT_OF_MEMORY); }
     if (hipMalloc(&s->d_lut, 512*sizeof(float)) != hipSuccess) { set_error("hipMalloc lut"); return fail(RT_ERROR_OUT_OF_MEMORY); }
     *out = s;
     return RT_OK;
@@ -4213,8 +4146,7 @@ int rt_scene_free(rt_scene* s) {
     if (s->d_samp) (void)hipFree(s->d_samp);
     if (s->d_samp_jy) (void)hipFree(s->d_samp_jy);
     if (s->d_lut) (void)hipFree(s->d_lut);
-    if (s->d_fs) (void)hipFree(s->d_fs);
-    if (s->h_fs) (void)hipHostFree(s->h_fs);
+    if (s->d_partials) (void)hipFree(s->d_partials);
     if (s->d_aux) (void)hipFree(s->d_aux);
     delete s;
     return RT_OK;
@@ -4391,23 +4323,23 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         if (sp.mode == RT_SPLAT_STREAM && ks > 12)
             sp.mode = (!by_pass && (double)total*20.0 <= budget) ? RT_SPLAT_EXACT : RT_SPLAT_ATOMIC;
         if (sp.mode == RT_SPLAT_STREAM) {
-            // a resolve every ~32M samples, and at least four per partition's share of the passes (a
-            // small shard, e.g. one rank's eighth of a frame, would otherwise resolve all its passes
-            // after its drain); the frame's one ring holds the passes not yet resolved: the chunk, the
-            // claims of the iterations a path can live (about 5 fills of every partition's pool) and slack
+            // a resolve every ~32M samples, and at least four per partition (a small shard, e.g. one
+            // rank's eighth of a frame, would otherwise resolve all its passes after its drain); the
+            // ring holds the passes not yet resolved: the chunk, the claims of the iterations a path
+            // can live (about 5 pool fills) and slack
             const uint32_t per_part = (spp + shape.nparts - 1) / shape.nparts;
             sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull),
                                                                std::max(1u, per_part / 4));
             if (s->cfg.splat_chunk > 0) sp.chunk = (uint32_t)s->cfg.splat_chunk;
-            const unsigned long long lag = (5ull*shape.pool_n*(unsigned)shape.nparts + fp.pixels - 1) / fp.pixels;
-            sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, spp);
+            const unsigned long long lag = (5ull*shape.pool_n + fp.pixels - 1) / fp.pixels;
+            sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, per_part);
             if (s->cfg.splat_ring > 0) sp.ring = (uint32_t)s->cfg.splat_ring;
             sp.chunk = std::min(sp.chunk, sp.ring);                   // the planner needs chunk <= ring
-            while (sp.ring > 1 && 20.0*(double)sp.ring*fp.pixels > budget) {
+            while (sp.ring > 1 && 20.0*(double)shape.nparts*sp.ring*fp.pixels > budget) {
                 sp.ring = std::max(1u, sp.ring / 2);
                 sp.chunk = std::min(sp.chunk, sp.ring);
             }
-            need_rec = (size_t)sp.ring*fp.pixels;
+            need_rec = (size_t)shape.nparts*sp.ring*fp.pixels;
             if (20.0*(double)need_rec > budget) { sp.mode = RT_SPLAT_ATOMIC; need_rec = 0; }
         }
         if (sp.mode == RT_SPLAT_EXACT) need_rec = (size_t)total;
@@ -4446,6 +4378,15 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         if (sp.mode == RT_SPLAT_STREAM) {
             sp.ksmax = ks <= 2 ? 2 : ks <= 4 ? 4 : 12;
             sp.lds = tr_lds_bytes(sp.ksmax);
+            const size_t npx = (size_t)w*h;
+            const size_t parts = (size_t)std::max(shape.nparts - 1, 0);
+            if (parts && s->partial_cap < parts*npx) {
+                if (s->d_partials) (void)hipFree(s->d_partials);
+                s->d_partials = nullptr; s->partial_cap = 0;
+                HIP_OK(hipMalloc(&s->d_partials, sizeof(float4)*parts*npx));
+                s->partial_cap = parts*npx;
+            }
+            sp.partials = s->d_partials;
             if (L.blocks_ks != ks) {
                 // output blocks whose source region (the block + the filter radius) meets an owned tile
                 std::vector<uint32_t> blocks;
@@ -4480,19 +4421,27 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
                         for (int x = 0; x < NXCD; ++x)
                             if (start[x] + k < start[x + 1]) blocks.push_back(colmajor[start[x] + k]);
                 }
-                const size_t aux = blocks.size();
+                const size_t aux = blocks.size() + 2*MAX_PARTITIONS;       // the pointer table, then the blocks
                 if (s->aux_cap < aux) {
                     if (s->d_aux) (void)hipFree(s->d_aux);
                     s->d_aux = nullptr; s->aux_cap = 0;
                     HIP_OK(hipMalloc(&s->d_aux, sizeof(uint32_t)*aux));
                     s->aux_cap = aux;
+                    L.aux_parts = -1;
                 }
-                HIP_OK(hipMemcpy(s->d_aux, blocks.data(), sizeof(uint32_t)*blocks.size(), hipMemcpyHostToDevice));
+                HIP_OK(hipMemcpy(s->d_aux + 2*MAX_PARTITIONS, blocks.data(), sizeof(uint32_t)*blocks.size(), hipMemcpyHostToDevice));
                 L.nblocks = (uint32_t)blocks.size();
                 L.blocks_ks = ks;
             }
+            if (L.aux_parts != (int)parts || L.aux_partials != s->d_partials || L.aux_npx != npx) {
+                std::vector<const float4*> part_ptrs;
+                for (size_t k = 0; k < parts; ++k) part_ptrs.push_back(s->d_partials + k*npx);
+                if (parts) HIP_OK(hipMemcpy(s->d_aux, part_ptrs.data(), sizeof(float4*)*parts, hipMemcpyHostToDevice));
+                L.aux_parts = (int)parts; L.aux_partials = s->d_partials; L.aux_npx = npx;
+            }
             sp.nblocks = L.nblocks;
-            sp.blocks = s->d_aux;
+            sp.blocks = s->d_aux + 2*MAX_PARTITIONS;
+            sp.part_ptrs = reinterpret_cast<const float4* const*>(s->d_aux);
             static bool attr_set = false;
             if (!attr_set) {                      // k_resolve_tiles<12> stages up to 72 KB
                 HIP_OK(hipFuncSetAttribute((const void*)k_resolve_tiles<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tr_lds_bytes(2)));

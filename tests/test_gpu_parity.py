@@ -241,28 +241,6 @@ def test_stream_splat_deterministic_in_chunking(c3small, env):
     assert np.array_equal(ref, got)
 
 
-@pytest.mark.parametrize("parts", [2, 3, 4])
-def test_stream_splat_independent_of_partitions(c3small, parts):
-    """r05: the partitions reserve their claims from one queue (FrameShared, the reference's atomic
-    tile queue, RT/raytracer.cpp:551-560) and the streaming splat resolves the frame's passes into the
-    caller's buffer in pass order, one resolve at a time: the frame is bit-identical whatever the
-    number of partitions or which of them rendered a sample (and run to run), with the same ray
-    counts.  At 192x108 and 512 spp the frame is large enough for four partitions (frame_shape)."""
-    rt, scene, cam, st, fc, dev = c3small
-    st = type(st).from_buffer_copy(st)
-    st.samples_per_pixel = 512
-    with dev.configured(partitions=1):
-        one, s1 = dev.render(cam, st, fc, 192, 108)
-    with dev.configured(partitions=parts):
-        got, sg = dev.render(cam, st, fc, 192, 108)
-        again, _ = dev.render(cam, st, fc, 192, 108)
-    REPORT[f"stream_partitions_{parts}"] = {"frame_equal_one_partition": bool(np.array_equal(one, got)),
-                                            "iterations": [int(s1.iterations), int(sg.iterations)]}
-    assert (sg.closest_hit_rays, sg.shadow_rays, sg.samples) == (s1.closest_hit_rays, s1.shadow_rays, s1.samples)
-    assert np.array_equal(got, again)
-    assert np.array_equal(one, got)
-
-
 def test_stream_splat_box_filter_bit_exact(c1):
     """With one partition the streaming splat of the box filter adds each pixel's samples in
     sample order, the reference's order: bit-identical to the oracle's frame."""
