@@ -137,7 +137,8 @@ class Stats(C.Structure):
                 ("iterations", C.c_uint64), ("seconds", C.c_double),
                 ("kernel_ms", C.c_double * RT_KERNEL_COUNT), ("kernel_launches", C.c_uint64 * RT_KERNEL_COUNT),
                 ("traced_rays", C.c_uint64 * 2), ("splat_mode", C.c_int32), ("reserved", C.c_int32),
-                ("traversal", TraversalStats * 2), ("trace_steps", C.c_uint64 * 2)]
+                ("traversal", TraversalStats * 2), ("trace_steps", C.c_uint64 * 2),
+                ("traversal_ref", TraversalStats * 2)]       # ABI 7: rt_scene_config::traversal_ref
 
     def traversal_total(self):
         """The reference's TraversalStats: both query kinds summed."""
@@ -150,7 +151,8 @@ class Stats(C.Structure):
                 "kernel_launches": {RT_KERNEL_NAMES[i]: self.kernel_launches[i] for i in range(6)},
                 "traced_rays": [self.traced_rays[0], self.traced_rays[1]], "splat_mode": self.splat_mode,
                 "traversal": [self.traversal[0].as_dict(), self.traversal[1].as_dict()],
-                "trace_steps": [self.trace_steps[0], self.trace_steps[1]]}
+                "trace_steps": [self.trace_steps[0], self.trace_steps[1]],
+                "traversal_ref": [self.traversal_ref[0].as_dict(), self.traversal_ref[1].as_dict()]}
 
 
 class RayQuery(C.Structure):
@@ -173,7 +175,8 @@ class SceneConfig(C.Structure):       # rt_scene_config (per-scene schedule and 
     _fields_ = [("splat_mode", C.c_int32), ("shard_mode", C.c_int32), ("env_sampling", C.c_int32),
                 ("partitions", C.c_int32), ("path_pool", C.c_int64), ("fuse_paths", C.c_int64),
                 ("splat_chunk", C.c_int32), ("splat_ring", C.c_int32), ("sample_budget_gb", C.c_double),
-                ("resolve_tall_pixels", C.c_int64), ("debug_traversal", C.c_int32), ("reserved", C.c_int32 * 7)]
+                ("resolve_tall_pixels", C.c_int64), ("debug_traversal", C.c_int32), ("traversal_ref", C.c_int32),
+                ("reserved", C.c_int32 * 6)]
 
 
 class BvhInfo(C.Structure):

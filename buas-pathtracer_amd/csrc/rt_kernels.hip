@@ -85,6 +85,9 @@ struct DevScene {
     const rt_bvh_node* mnodes;      // all mesh BVH nodes (child indices mesh-local), traversal layout
     const rt_bvh_node* mnodes_src;  // the same in the caller's layout
     const float4* mnodes4;          // mesh BVH4 nodes (MESH_BVH4), 8 float4 each, global indices
+    // per BVH4 node: the boxes of the BVH2 node's two children (the level the BVH4 skips), 3 float4:
+    // {pL.xyz, rL.x}, {rL.yz, pR.xy}, {pR.z, rR.xyz} -- read only when counting in the reference's units
+    const float4* mid4;
     const float* sky;               // 3 floats per pixel
     uint32_t sky_w, sky_h;
     // environment-map sampling table (rt_set_env_sampling): per luma tile {alias threshold,
@@ -411,6 +414,9 @@ constexpr uint32_t TRI_FETCH = 2;
 // level in between is skipped, i.e. its box test, which only culls what its
 // children's own tests cull (their boxes lie inside it).  Halves the interior steps.
 constexpr uint32_t EMPTY4 = 0xFFFFFFFFu;
+// a stack entry that is no node: a skipped BVH2 level's far child, counted when popped (Traversal::rp,
+// reference units only).  As an index form it would name node 0x7FFFFFFE, which no BVH has.
+constexpr uint32_t REF_MARKER = 0xFFFFFFFEu;
 constexpr int FETCH_Q = 8;                       // float4 per lane per step: one 128-byte BVH4 node
 
 // The part of intersect_scene_internal (RT/intersection.cpp:411-598) that needs
@@ -558,7 +564,10 @@ struct StepField {
 // TraversalStats counters of a partition: per ray kind (0 closest, 1 shadow) and shard, TV_* counts.
 // TV_DRAIN: the fused drain's steps (entries + nodes + triangle fetches + top level), which the
 // others include too: trace_steps leaves them out (rt_stats::trace_steps, the extend / connect launches')
-enum { TV_ENTRIES, TV_NODES, TV_LEAVES, TV_TRIS, TV_TOP, TV_CALLS, TV_DRAIN, TV_N = 8 };
+// TV_REF_*: rt_scene_config::traversal_ref, the reference's own units (rt_stats::traversal_ref): BVH2
+// nodes taken from the stack, interior nodes and leaves passing their pop-time test
+enum { TV_ENTRIES, TV_NODES, TV_LEAVES, TV_TRIS, TV_TOP, TV_CALLS, TV_DRAIN, TV_REF_TRAV, TV_REF_NODE, TV_REF_LEAF,
+       TV_N = 12 };
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 // A wave's step counts.  flush(acc), at a point every lane of the wave reaches, sums the lanes'
 // Traversal::acc (StepField) over the wave with DPP reductions, two fields per reduction (64 x 255
@@ -580,6 +589,12 @@ struct StepCounts {
         acc = 0;
     }
     RT_D void check(uint32_t& acc) { if (__ballot((acc & F::HI) != 0u)) flush(acc); }
+    // the reference-unit counts (Traversal::rc, rt_scene_config::traversal_ref), summed over the wave
+    unsigned long long ref[3] = {0, 0, 0};
+    RT_D void flush_ref(uint32_t (&rc)[3]) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) { ref[i] += __ockl_wfred_add_u32(rc[i]); rc[i] = 0; }
+    }
     // drain: k_drain's counts, also added to TV_DRAIN as steps
     RT_D void commit(unsigned long long* trav, int kind, bool drain = false) const {
         if (__lane_id() != (uint32_t)(__ffsll((long long)__ballot(true)) - 1)) return;
@@ -588,11 +603,16 @@ struct StepCounts {
             if (tot[i]) atomicAdd(&trav[kind*TV_N + i], (unsigned long long)tot[i]);
         const unsigned long long st = (unsigned long long)tot[TV_ENTRIES] + tot[TV_NODES] + tot[TV_TRIS] + tot[TV_TOP];
         if (drain && st) atomicAdd(&trav[kind*TV_N + TV_DRAIN], st);
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+            if (ref[i]) atomicAdd(&trav[kind*TV_N + TV_REF_TRAV + i], ref[i]);
     }
 };
 
-template <bool OCC, bool LST = false, int SL = STACK_LDS>
+// REF: count the reference's TraversalStats units too (rt_scene_config::traversal_ref; top-level walks only)
+template <bool OCC, bool LST = false, int SL = STACK_LDS, bool REF = false>
 struct Traversal {
+    static_assert(!(REF && LST), "reference units need the reference's top-level walk");
     using Stack = StackT<SL>;
     V3 wo, wd;          // world ray
     V3 co, cd, cinv;    // current ray (object space while in a mesh)
@@ -609,6 +629,12 @@ struct Traversal {
     uint32_t inst, node_off, tri_off;   // TM_MESH: the instance
     uint32_t cur_lf, cur_cnt, cur_ax;   // node held by the lane (cur_cnt: leaf size, 0 interior)
     bool has_cur, occluded, finite_world;
+    // rt_scene_config::traversal_ref (REF; top-level walks only): the reference's
+    // TraversalStats of the current mesh instance in its own units -- [0] BVH2 nodes taken from the stack,
+    // [1] interior nodes and [2] leaves passing their pop-time test (RT/intersection.cpp:274-380) -- and
+    // those committed: an instance's counts are committed when its walk ends, and dropped when a shadow
+    // query ends inside it (the reference returns before adding them, :297-299)
+    uint32_t rp[3] = {0, 0, 0}, rc[3] = {0, 0, 0};
 
     RT_D Ray cur_ray() const {
         Ray r; r.o = co; r.d = cd; r.inv_d = cinv; r.neg = cflags & 7u; r.zero = cflags >> 3; r.max_t = 0.0f;
@@ -692,6 +718,10 @@ struct Traversal {
     RT_D bool pop(const Stack& st, const rt_bvh_node* nodes, int base) {
         while (sp > base) {
             const uint2 e = st.template get<SH>(--sp);
+            if (REF && e.x == REF_MARKER) {              // a skipped BVH2 level's far child (push_children4)
+                if (__uint_as_float(e.y) < t) { rp[0] += 2u; rp[1] += 1u; }
+                continue;
+            }
             if (__uint_as_float(e.y) < t) {
                 unpack_node(nodes, e.x, cur_lf, cur_cnt, cur_ax);
                 has_cur = true;
@@ -703,7 +733,7 @@ struct Traversal {
 
     // children of a mesh BVH4 node F[0..7], pushed so they pop in the BVH2 depth-first order
     template <bool SH, bool FIN>
-    RT_D void push_children4(const Stack& st, const float4* F) {
+    RT_D void push_children4(const Stack& st, const float4* F, const float4* mid = nullptr) {
         const Ray r = cur_ray();
         const uint32_t meta = __float_as_uint(F[7].x), nb = cflags & 7u;
         const uint32_t g = (nb >> (meta & 3u)) & 1u;               // group visited first: 1 = the right pair
@@ -719,6 +749,26 @@ struct Traversal {
         // visit order: first pair (2g + its first, 2g + its second), then the other pair; push reversed
         const uint32_t f1 = g ? fb : fa, f2 = g ? fa : fb;
         const uint32_t v[4] = {2u*g + f1, 2u*g + 1u - f1, 2u*(1u - g) + f2, 2u*(1u - g) + 1u - f2};
+        // Reference units (rt_scene_config::traversal_ref): this node passed its pop-time test and the
+        // reference pops both its children; each child that is interior (its pair's second slot is
+        // used) pops its own two when it passes -- the near one now (nothing changes t before the
+        // reference pops it), the far one when a marker pushed below the near pair's entries is popped
+        // (t then holds whatever the near subtree found).
+        bool far_marker = false;
+        float far_tn = 0.0f;
+        if (REF) {
+            rp[0] += 2u; rp[1] += 1u;
+            const V3 pc[2] = {{mid[0].x, mid[0].y, mid[0].z}, {mid[1].z, mid[1].w, mid[2].x}};
+            const V3 rr[2] = {{mid[0].w, mid[1].x, mid[1].y}, {mid[2].y, mid[2].z, mid[2].w}};
+#pragma unroll
+            for (uint32_t c = 0; c < 2; ++c) {
+                if ((c == 0 ? rec[1] : rec[3]) == EMPTY4) continue;           // a leaf child: counted when popped
+                float tc;
+                const bool hc = bv_static<FIN>(r, pc[c], rr[c], tc);
+                if (c == g) { if (hc && tc < t) { rp[0] += 2u; rp[1] += 1u; } }
+                else if (hc) { far_marker = true; far_tn = tc; }
+            }
+        }
 #pragma unroll
         for (int k = 3; k >= 0; --k) {
             const uint32_t i = v[k];
@@ -726,6 +776,7 @@ struct Traversal {
             const uint32_t ri = i == 0 ? rec[0] : i == 1 ? rec[1] : i == 2 ? rec[2] : rec[3];
             const float ti = i == 0 ? tn[0] : i == 1 ? tn[1] : i == 2 ? tn[2] : tn[3];
             if (hi) push<SH>(st, ri, ti);
+            if (REF && k == 2 && far_marker) push<SH>(st, REF_MARKER, far_tn);
         }
     }
 
@@ -733,7 +784,7 @@ struct Traversal {
     // step fetched is added to `acc` (StepField, the lane's TraversalStats counts since the last flush).
     // A step pops before it pushes and pushes at most PUSH_MAX entries, so when no lane of
     // the wave is within PUSH_MAX levels of STACK_LDS the whole step stays in LDS.
-    static constexpr int PUSH_MAX = 4;
+    static constexpr int PUSH_MAX = REF ? 5 : 4;       // REF: a far-child marker beside the four children
     using SF = StepField<LST>;
     uint32_t acc = 0;                   // SF fields of the steps since the caller last flushed them
     RT_D bool step(const DevScene& sc, const Stack& st) {
@@ -762,6 +813,7 @@ struct Traversal {
         const bool take = mode == TM_MESH && !has_cur;
         if (take && !pop<SH>(st, sc.mnodes_src + node_off, LST ? 0 : mesh_base)) {
             mode = TM_LEAF;                                        // instance finished
+            if (REF) { rc[0] += rp[0]; rc[1] += rp[1]; rc[2] += rp[2]; rp[0] = rp[1] = rp[2] = 0u; }
             // LST: the next step is the end or a listed instance's leaf step, which sets the
             // object-space ray from wo / wd itself (nothing reads the world ray in between)
             if (!LST) set_world();
@@ -803,12 +855,16 @@ struct Traversal {
             // LST: the prologue lists mesh instances only (spheres and boxes were tested there)
             if (LST || type == RT_PRIMITIVE_MESH) {               // intersect_mesh :243-401
                 co = ir.o; cd = ir.d; cinv = ir.inv_d;
-                cflags = ir.neg | (ir.zero << 3) | ((sc.finite_boxes && finite_box_ray(ir.o, ir.inv_d)) ? 64u : 0u);
+                // (reference units: no degenerate-axis pruning, so the walk visits the reference's nodes)
+                cflags = ir.neg | (REF ? 0u : ir.zero << 3) | ((sc.finite_boxes && finite_box_ray(ir.o, ir.inv_d)) ? 64u : 0u);
+                if (REF) { rp[0] = 1u; rp[1] = 0u; rp[2] = 0u; }    // the reference pops the root (:266-274)
                 inst = pi; node_off = __float_as_uint(F[3].z); tri_off = __float_as_uint(F[3].w);
                 if (!LST) mesh_base = sp;              // LST: the stack holds this mesh only
                 const V3 rp = {F[4].y, F[4].z, F[4].w}, rr = {F[5].x, F[5].y, F[5].z};
                 float tn;
-                if (bv_static(ir, rp, rr, tn)) push<SH>(st, __float_as_uint(F[4].x), tn);
+                Ray rr_ = ir;
+                if (REF) rr_.zero = 0u;                            // reference units: no pruning at the root either
+                if (bv_static(rr_, rp, rr, tn)) push<SH>(st, __float_as_uint(F[4].x), tn);
                 mode = TM_MESH;
                 acc += SF::ENTRY;
                 return true;
@@ -827,6 +883,7 @@ struct Traversal {
         }
         if (cur_cnt) {                                             // mesh leaf: triangles in order
             acc += fresh ? (SF::LEAF | SF::TRIS) : SF::TRIS;
+            if (REF && fresh) rp[2] += 1u;
             Ray r; r.o = co; r.d = cd;
             const uint32_t g0 = tri_off + cur_lf;
             float bv = 0.0f, bw = 0.0f;
@@ -846,7 +903,11 @@ struct Traversal {
             return true;
         }
         has_cur = false;
-        if (LST || mode == TM_MESH) { push_children4<SH, FIN>(st, F); acc += SF::NODE; return true; }
+        if (LST || mode == TM_MESH) {
+            push_children4<SH, FIN>(st, F, REF ? sc.mid4 + 3*(size_t)cur_lf : nullptr);
+            acc += SF::NODE;
+            return true;
+        }
         push_children<SH, FIN>(st, F);
         if (!LST) acc += SF::TOP;
         return true;
@@ -1701,13 +1762,13 @@ constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 // 90 / 86 VGPRs without spills (r05: 96 before the step split), which leaves room for two 64-VGPR k_shade waves beside four
 // trace waves instead of one (the 112-VGPR build).  The top-level builds keep the 4-wave
 // budget (118 / 114 VGPRs; at 96 they spill).
-#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LST ? 5 : 4)))
+#define RT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(LST ? 5 : REF ? 3 : 4)))   // REF: the diagnostic reference-unit walk
 constexpr int TRACE_STACK_LDS = STACK_LDS;
 constexpr size_t TRACE_LDS = sizeof(uint2)*TRACE_STACK_LDS*TB + sizeof(float2)*TB;   // dynamic, per block
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
-template <bool OCC, bool LST>
+template <bool OCC, bool LST, bool REF = false>
 __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill,
                                                               int fuse) {
     if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
@@ -1730,7 +1791,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     uint32_t chunk_next = 0, chunk_end = 0;
     bool exhausted = false, active = false;
     uint32_t item = 0;
-    Traversal<OCC, LST, TRACE_STACK_LDS> tr;
+    Traversal<OCC, LST, TRACE_STACK_LDS, REF> tr;
     StepCounts<LST> tally;                              // checked after every refill round
     static_assert(STEPS_PER_REFILL <= StepField<LST>::MARGIN, "StepCounts: a round's steps fit a field's upper half");
     auto finish = [&]() {
@@ -1798,6 +1859,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
         tally.check(tr.acc);                            // every lane is here
     }
     tally.flush(tr.acc);
+    if (REF) tally.flush_ref(tr.rc);
     tally.commit(cnt->trav[blockIdx.x % NSHARD], OCC ? 1 : 0);
 }
 
@@ -2225,7 +2287,7 @@ __global__ void __launch_bounds__(BLOCK) k_drain_list(Pool pool, Counters* cnt) 
 // the other partitions' kernels (those empty launches cost up to ~1 ms each in the iterations before
 // the drain).
 constexpr int DTB = 64;
-template <bool LST, bool ENV>
+template <bool LST, bool ENV, bool REF = false>
 __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
                                                uint2* spill) {
     if (!cnt->fused || cnt->done) return;                              // uniform
@@ -2311,7 +2373,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
         Hit h;
         h.t = pro.t; h.code = pro.code; h.tri = 0; h.v = 0.0f; h.w = 0.0f;
         {
-            Traversal<false, LST> tr;
+            Traversal<false, LST, STACK_LDS, REF> tr;
             bool tracing = active && pro.bvh;
             if (tracing) {
                 tr.init_rec(sc, stk, ro, rd, pro.inv_d, pro.t, 0u, pro.mlist);
@@ -2322,6 +2384,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                 if (k % StepField<LST>::H == 0) tally[0].flush(tr.acc);   // one step per lane per k
             }
             tally[0].flush(tr.acc);
+            if (REF) tally[0].flush_ref(tr.rc);
             if (active && pro.bvh && tr.code != RT_HIT_MISS) h = tr.result(stk);
         }
         // one bounce
@@ -2341,7 +2404,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
             Prologue spro = {};
             if (cast_shadow) spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
             n_calls[1] += cast_shadow ? spro.calls : 0u;
-            Traversal<true, LST> tr;
+            Traversal<true, LST, STACK_LDS, REF> tr;
             bool tracing = cast_shadow && !spro.occluded && spro.bvh;
             n_traced_sh += tracing ? 1u : 0u;
             if (tracing) {
@@ -2353,6 +2416,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                 if (k % StepField<LST>::H == 0) tally[1].flush(tr.acc);   // one step per lane per k
             }
             tally[1].flush(tr.acc);
+            if (REF) tally[1].flush_ref(tr.rc);
             if (cast_shadow && !spro.occluded && (!spro.bvh || !tr.occluded)) total = add(total, sh_c);
         }
         n_shadow += cast_shadow ? 1u : 0u;
@@ -3003,6 +3067,7 @@ struct rt_scene {
     } layout;
     volatile int cancel = 0;
     uint32_t bvh_depth = 0;
+    uint32_t bvh_depth_ref = 0;         // stack entries a reference-unit walk (with markers) may hold
     rt_scene_config cfg = {};           // rt_scene_set_config; read at every frame, never the environment
 };
 
@@ -3077,10 +3142,13 @@ std::vector<float4> top_sequences(const rt_bvh_node* nodes, uint32_t count, uint
 // records are global BVH4 indices (`base` + local); leaves keep the BVH2 packed
 // record (or its index form, mesh-local).  `need` = an upper bound of the stack
 // entries a traversal below this node can hold.  Returns the node's record.
+// src (optional): the BVH2 node each BVH4 node was built from, by BVH4 index (mid4's boxes).
+// levels: the BVH4 levels below and including this node (a reference-unit walk's markers, need_ref).
 uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, std::vector<float4>& out,
-                    uint32_t& need, bool& ok) {
+                    uint32_t& need, bool& ok, std::vector<uint32_t>* src = nullptr, uint32_t* levels = nullptr) {
     const uint32_t k = (uint32_t)(out.size() / 8);
     out.resize(out.size() + 8, make_float4(0, 0, 0, 0));
+    if (src) { src->resize(k + 1); (*src)[k] = i; }
     uint32_t slot[4] = {EMPTY4, EMPTY4, EMPTY4, EMPTY4};
     uint32_t meta = n[i].split_axis & 3u;
     auto interior = [&](uint32_t c) { return n[c].count == 0 && n[c].left_first != 0 && n[c].left_first + 1 < count; };
@@ -3097,7 +3165,7 @@ uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, std::vecto
     }
     float4 q[8];
     for (int j = 0; j < 8; ++j) q[j] = make_float4(0, 0, 0, 0);
-    uint32_t nchild = 0, deeper = 0;
+    uint32_t nchild = 0, deeper = 0, lv = 0;
     for (int j = 0; j < 4; ++j) {
         uint32_t rec = EMPTY4;
         if (slot[j] != EMPTY4) {
@@ -3107,9 +3175,10 @@ uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, std::vecto
             (&q[3].x)[j] = c.bv_r.x; (&q[4].x)[j] = c.bv_r.y; (&q[5].x)[j] = c.bv_r.z;
             ++nchild;
             if (interior(m)) {
-                uint32_t cn = 0;
-                rec = build_bvh4(n, count, m, out, cn, ok);
+                uint32_t cn = 0, cl = 0;
+                rec = build_bvh4(n, count, m, out, cn, ok, src, &cl);
                 deeper = std::max(deeper, cn);
+                lv = std::max(lv, cl);
             } else {
                 rec = pack_node(m, c.left_first, c.count, 0);
                 if (!(rec & 0x80000000u) && !((rec >> 30) & 1u)) rec = 0x80000000u | m;   // never an interior form
@@ -3120,6 +3189,7 @@ uint32_t build_bvh4(const rt_bvh_node* n, uint32_t count, uint32_t i, std::vecto
     memcpy(&q[7].x, &meta, 4);
     for (int j = 0; j < 8; ++j) out[8*(size_t)k + j] = q[j];
     need = (nchild ? nchild - 1 : 0) + deeper;
+    if (levels) *levels = lv + 1;
     if (k >= (1u << 28)) ok = false;
     return k;                       // out holds every mesh's nodes: k is already the global index
 }
@@ -3433,6 +3503,11 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         }
     };
     // environment-map NEE (rt_set_env_sampling): only with a map, its table and NEE
+    // rt_scene_config::traversal_ref: the trace kernels walk the top level in the reference's order (no
+    // prologue sequence: the prologue tests the planes and the root only) and count the reference's units
+    const bool ref = s->cfg.traversal_ref > 0;
+    DevScene ds = s->ds;
+    if (ref) { ds.top_seq = nullptr; ds.top_seq_len = 0; ds.listed_only = 0; }
     const bool env = (s->cfg.env_sampling >= 0 ? s->cfg.env_sampling : g_env_sampling) && s->ds.env_tab &&
                      st->next_event_estimation;
     auto iterate = [&](int k, bool plan) {
@@ -3448,33 +3523,38 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         // iteration after k_bookkeep set Counters::fused, whose extend / shade / connect then exit
         const int fuse = (r.near && fuse_paths) ? 1 : 0;
         b(RT_KERNEL_GENERATE);
-        k_generate<<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur);
+        k_generate<<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE);
         if (fuse) {
             k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
-            if (s->ds.listed_only) {
-                if (env) k_drain<true, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-                else k_drain<true, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+            if (ds.listed_only) {
+                if (env) k_drain<true, true><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<true, false><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
+            } else if (ref) {
+                if (env) k_drain<false, true, true><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<false, false, true><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
             } else {
-                if (env) k_drain<false, true><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
-                else k_drain<false, false><<<s->drain_grid, DTB, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, pt.spill);
+                if (env) k_drain<false, true><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
+                else k_drain<false, false><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
             }
         }
         b(RT_KERNEL_EXTEND);
-        if (s->ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else k_trace<false, false><<<s->trace_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        if (ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else if (ref) k_trace<false, false, true><<<s->trace_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else k_trace<false, false><<<s->trace_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
         if (env) {
-            if (s->ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
-            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
-        } else if (s->ds.blob_q) {
-            k_shade<true, false><<<r.grid, BLOCK, 16*s->ds.blob_q, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
+            if (ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*ds.blob_q, q>>>(ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
+            else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
+        } else if (ds.blob_q) {
+            k_shade<true, false><<<r.grid, BLOCK, 16*ds.blob_q, q>>>(ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         } else {
-            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(s->ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
+            k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         }
         e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (s->ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else k_trace<true, false><<<s->connect_grid, TB, TRACE_LDS, q>>>(s->ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        if (ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else if (ref) k_trace<true, false, true><<<s->connect_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
+        else k_trace<true, false><<<s->connect_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
         e(RT_KERNEL_CONNECT);
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
@@ -3601,7 +3681,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         const unsigned long long* v = tv + a*TV_N;
         // the prologue's walk reaches the instances (ray_prologue); a scene whose top level is too large
         // for the prologue has it walked by the trace kernels, whose entries are then the calls
-        ts[a].mesh_intersection_count = s->ds.top_seq ? v[TV_CALLS] : v[TV_ENTRIES];
+        ts[a].mesh_intersection_count = (s->ds.top_seq && !ref) ? v[TV_CALLS] : v[TV_ENTRIES];
         ts[a].mesh_bvh_traversals = v[TV_ENTRIES] + v[TV_NODES] + v[TV_TRIS];
         ts[a].mesh_node_traversals = v[TV_NODES];
         ts[a].mesh_leaf_traversals = v[TV_LEAVES];
@@ -3628,6 +3708,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         for (int a = 0; a < 2; ++a) {
             stats->traversal[a] = ts[a];
             stats->trace_steps[a] = steps[a];
+            if (ref) {                                  // the reference's units (rt_scene_config::traversal_ref)
+                const unsigned long long* v = tv + a*TV_N;
+                stats->traversal_ref[a].mesh_intersection_count = v[TV_ENTRIES];
+                stats->traversal_ref[a].mesh_bvh_traversals = v[TV_REF_TRAV];
+                stats->traversal_ref[a].mesh_node_traversals = v[TV_REF_NODE];
+                stats->traversal_ref[a].mesh_leaf_traversals = v[TV_REF_LEAF];
+            }
         }
     }
     return RT_OK;
@@ -3741,6 +3828,7 @@ int check_config(const rt_scene_config* c) {
     else if (c->splat_chunk < 0 || c->splat_ring < 0) bad = "splat_chunk / splat_ring";
     else if (!(c->sample_budget_gb == c->sample_budget_gb)) bad = "sample_budget_gb";
     else if (c->resolve_tall_pixels < 0) bad = "resolve_tall_pixels";
+    else if (c->traversal_ref != 0 && c->traversal_ref != 1) bad = "traversal_ref";
     if (bad) { set_error(std::string("rt_scene_config: bad ") + bad); return RT_ERROR_INVALID; }
     return RT_OK;
 }
@@ -3785,6 +3873,7 @@ bool config_from_env(rt_scene_config& c) {
     }
     if (num("RT_RES_TALL_PIXELS", 0, 1ll << 40, v)) c.resolve_tall_pixels = v;
     if (num("RT_DEBUG_TRAVERSAL", 0, 1, v)) c.debug_traversal = (int32_t)v;
+    if (num("RT_TRAVERSAL_REF", 0, 1, v)) c.traversal_ref = (int32_t)v;
     return ok;
 }
 
@@ -3808,6 +3897,10 @@ int rt_scene_set_config(rt_scene* s, const rt_scene_config* c) {
     if (!s || !c) { set_error("null argument"); return RT_ERROR_INVALID; }
     int err = check_config(c);
     if (err) return err;
+    if (c->traversal_ref && s->bvh_depth_ref + 2 > STACK_DEPTH) {
+        set_error("rt_scene_config: traversal_ref needs more than the 64-entry traversal stack for this BVH");
+        return RT_ERROR_INVALID;
+    }
     s->cfg = *c;
     memset(s->cfg.reserved, 0, sizeof(s->cfg.reserved));
     return RT_OK;
@@ -3934,6 +4027,9 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
     uint32_t mesh_depth = 0;
     std::vector<float4> mnodes4;
     std::vector<uint32_t> root4(d->mesh_count, 0u);
+    std::vector<uint32_t> src4;                 // BVH4 node -> its BVH2 node (mesh-local)
+    std::vector<uint32_t> mesh4(1, 0u);         // BVH4 nodes before mesh m's
+    uint32_t mesh_depth_ref = 0;                // mesh_depth with a reference-unit walk's markers
     for (uint32_t m = 0; m < d->mesh_count; ++m) {
         const rt_mesh& M = d->meshes[m];
         meshes[m].tri_offset = (uint32_t)orig.size();
@@ -3952,10 +4048,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 mesh_depth = std::max(mesh_depth, 1u);
             } else {
                 bool ok = true;
-                uint32_t need = 0;
-                root4[m] = build_bvh4(M.nodes, M.node_count, 0u, mnodes4, need, ok);
+                uint32_t need = 0, levels = 0;
+                root4[m] = build_bvh4(M.nodes, M.node_count, 0u, mnodes4, need, ok, &src4, &levels);
                 if (!ok) { set_error("mesh BVH too large for the BVH4 records"); return fail(RT_ERROR_INVALID); }
                 mesh_depth = std::max(mesh_depth, need + 1);
+                mesh_depth_ref = std::max(mesh_depth_ref, need + 1 + levels);
             }
         }
         for (uint32_t t = 0; t < M.triangle_count; ++t) {
@@ -3975,6 +4072,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 normals.push_back(nn.x); normals.push_back(nn.y); normals.push_back(nn.z);
             }
         mnodes.insert(mnodes.end(), M.nodes, M.nodes + M.node_count);
+        mesh4.push_back((uint32_t)(mnodes4.size() / 8));
     }
     {   // finite_box_ray's scene condition: every box within 2^40 of the origin
         auto within = [](const rt_bvh_node* n, size_t count) {
@@ -3992,6 +4090,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         return fail(RT_ERROR_INVALID);
     }
     s->bvh_depth = top_depth + mesh_depth;
+    s->bvh_depth_ref = top_depth + std::max(mesh_depth, mesh_depth_ref);
+    if (s->cfg.traversal_ref && s->bvh_depth_ref + 2 > STACK_DEPTH) {       // RT_TRAVERSAL_REF
+        set_error("rt_scene_upload: traversal_ref needs more than the 64-entry traversal stack for this BVH");
+        return fail(RT_ERROR_INVALID);
+    }
     {   // top-level leaf records, in bvh_indices order
         auto u2f = [](uint32_t u) { float f; memcpy(&f, &u, 4); return f; };
         std::vector<float4> rec((size_t)d->bvh_index_count*LEAF_REC_Q, make_float4(0, 0, 0, 0));
@@ -4051,7 +4154,23 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             }
         if (bad) { set_error("internal: mesh BVH4 record out of range"); return fail(RT_ERROR_INVALID); }
     }
+    ds.mid4 = nullptr;
     if (!mnodes4.empty()) {
+        // mid4: per BVH4 node, the boxes of its BVH2 node's two children (the skipped level)
+        std::vector<float4> mid(3*(mnodes4.size() / 8), make_float4(0, 0, 0, 0));
+        for (uint32_t m = 0; m < d->mesh_count; ++m) {
+            const rt_mesh& M = d->meshes[m];
+            for (uint32_t k = mesh4[m]; k < mesh4[m + 1]; ++k) {
+                const uint32_t i = src4[k], l = M.nodes[i].left_first;
+                if (M.nodes[i].count || l + 1 >= M.node_count) continue;
+                const rt_bvh_node& L = M.nodes[l];
+                const rt_bvh_node& R = M.nodes[l + 1];
+                mid[3*k] = make_float4(L.bv_p.x, L.bv_p.y, L.bv_p.z, L.bv_r.x);
+                mid[3*k + 1] = make_float4(L.bv_r.y, L.bv_r.z, R.bv_p.x, R.bv_p.y);
+                mid[3*k + 2] = make_float4(R.bv_p.z, R.bv_r.x, R.bv_r.y, R.bv_r.z);
+            }
+        }
+        if ((err = upload(s, mid.data(), mid.size(), &ds.mid4))) return fail(err);
         mnodes4.resize(mnodes4.size() + FETCH_Q, make_float4(0, 0, 0, 0));
         if ((err = upload(s, mnodes4.data(), mnodes4.size(), &ds.mnodes4))) return fail(err);
     }

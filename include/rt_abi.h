@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 /* ---------------------------------------------------------------- status */
 enum rt_status {
@@ -260,6 +260,14 @@ typedef struct rt_stats {
        drain's steps, which the TraversalStats above include, are left out, so that the steps match the
        launches bench.py times): the fetch rounds of 128 B per lane the traversal roofline counts */
     uint64_t trace_steps[2];
+    /* (ABI 7) The reference's own TraversalStats units, filled only when rt_scene_config::traversal_ref
+       is set (zero otherwise): per query kind, intersect_mesh calls and the BVH2 counts of the
+       reference's walk -- nodes taken from the stack (RT/intersection.cpp:274), interior nodes (:358)
+       and leaves (:279) passing their pop-time test -- with its top-level order and its early return
+       (a shadow query that a mesh occludes adds no traversal counts, :297-299).  These are the numbers
+       the reference's UI prints (RT/raytracer.cpp:2050-2056); tests/test_gpu_fullscale.py holds them to
+       the oracle's reference walk of the same frame. */
+    rt_traversal_stats traversal_ref[2];
 } rt_stats;
 
 typedef struct rt_ray_query {       /* debug/parity entry: one ray for rt_debug_intersect */
@@ -469,7 +477,10 @@ typedef struct rt_scene_config {
     double   sample_budget_gb;      /* HBM for sample records; < 0 = auto (free HBM less 16 GB)      */
     int64_t  resolve_tall_pixels;   /* exact splat: 8-row gather strips from this many pixels; 0 = auto */
     int32_t  debug_traversal;       /* 1: each frame's TraversalStats and trace steps to stderr      */
-    int32_t  reserved[7];
+    int32_t  traversal_ref;         /* 1: also count rt_stats::traversal_ref (the reference's units);
+                                       the trace kernels then walk the top level in the reference's
+                                       order (slower: no prologue mesh lists) -- a diagnostic mode  */
+    int32_t  reserved[6];
 } rt_scene_config;
 int rt_scene_default_config(rt_scene_config* out);
 int rt_scene_get_config(const rt_scene* scene, rt_scene_config* out);

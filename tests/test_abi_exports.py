@@ -24,7 +24,7 @@ def test_every_declared_symbol_is_exported(rt):
     assert len(names) > 40
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.rt_abi_version() == 6
+    assert lib.rt_abi_version() == 7
 
 
 def test_ctypes_table_covers_header(rt):
@@ -42,7 +42,8 @@ def test_struct_sizes_match_reference_layout(rt):
 
 
 def test_stats_layout_matches_header(rt, tmp_path):
-    """The ctypes rt_stats (with the TraversalStats fields of ABI v6) has the C header's layout."""
+    """The ctypes rt_stats (the TraversalStats fields of ABI v6, the reference-unit ones of v7) has the
+    C header's layout."""
     import ctypes as C
     import shutil
     import subprocess
@@ -50,14 +51,16 @@ def test_stats_layout_matches_header(rt, tmp_path):
         pytest.skip("needs gcc")
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "rt_abi.h"\n'
-                   'int main(void) { printf("%zu %zu %zu %zu\\n", sizeof(rt_stats), offsetof(rt_stats, traversal), '
-                   'offsetof(rt_stats, trace_steps), sizeof(rt_traversal_stats)); return 0; }\n')
+                   'int main(void) { printf("%zu %zu %zu %zu %zu %zu\\n", sizeof(rt_stats), offsetof(rt_stats, traversal), '
+                   'offsetof(rt_stats, trace_steps), sizeof(rt_traversal_stats), offsetof(rt_stats, traversal_ref), '
+                   'offsetof(rt_scene_config, traversal_ref)); return 0; }\n')
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
-    size, off_trav, off_steps, tsize = map(int, subprocess.check_output([str(exe)]).split())
+    size, off_trav, off_steps, tsize, off_ref, off_cfg_ref = map(int, subprocess.check_output([str(exe)]).split())
     a = rt.abi
     assert C.sizeof(a.Stats) == size
     assert a.Stats.traversal.offset == off_trav and a.Stats.trace_steps.offset == off_steps
+    assert a.Stats.traversal_ref.offset == off_ref and a.SceneConfig.traversal_ref.offset == off_cfg_ref
     assert C.sizeof(a.TraversalStats) == tsize == 32
 
 
@@ -81,3 +84,4 @@ def test_scene_config_defaults(rt):
     assert (c.splat_mode, c.shard_mode, c.env_sampling) == (a.RT_CONFIG_INHERIT,) * 3
     assert (c.partitions, c.path_pool, c.fuse_paths, c.splat_chunk, c.splat_ring) == (0, 0, -1, 0, 0)
     assert c.sample_budget_gb < 0 and c.resolve_tall_pixels == 0 and c.debug_traversal == 0
+    assert c.traversal_ref == 0

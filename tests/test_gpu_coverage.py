@@ -12,6 +12,7 @@
 * frames sharded over 2, 4 and 8 ranks (tiles t % N) summing to the single-rank frame, in the
   streaming splat (each rank resolves only the blocks its tiles reach) and the exact one.
 """
+import os
 import threading
 
 import numpy as np
@@ -310,3 +311,29 @@ def test_bad_override_rejected(rt, monkeypatch, var, value):
     with pytest.raises(rt.RenderError) as e:
         rt.DeviceScene(scene, 0)
     assert e.value.code == rt.abi.RT_ERROR_INVALID and var in str(e.value)
+
+
+@pytest.mark.parametrize("preset", ["c3", "c4"])
+def test_traversal_ref_units(rt, preset):
+    """rt_scene_config::traversal_ref: the trace kernels walk the top level in the reference's order and
+    count TraversalStats in its BVH2 units (rt_stats::traversal_ref); against the reference's own counts
+    of the same frame (the oracle's reference walk) within 1e-3, the frame and ray counts unchanged."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("fullscale", os.path.join(os.path.dirname(__file__), "test_gpu_fullscale.py"))
+    fs = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(fs)
+    w, h = 320, 180
+    scene, cam, st, fc, post = rt.load_preset(preset, w, h)
+    st.samples_per_pixel = 16
+    dev = rt.DeviceScene(scene, 0)
+    try:
+        with dev.configured(traversal_ref=1):
+            gpu, gs = dev.render(cam, st, fc, w, h)
+        plain, ps = dev.render(cam, st, fc, w, h)
+    finally:
+        dev.close()
+    cpu, cs = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=8)
+    REPORT[f"traversal_ref_{preset}_{w}x{h}_16spp"] = fs.check_traversal_ref(gs, cs)
+    assert all(v == 0 for k in range(2) for v in ps.traversal_ref[k].as_dict().values())   # off: not counted
+    assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays) == (ps.closest_hit_rays, ps.shadow_rays)
+    assert rel_l2(gpu, cpu) <= 1e-5 and rel_l2(plain, cpu) <= 1e-5

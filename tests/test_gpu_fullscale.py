@@ -56,6 +56,10 @@ def test_full_frame_default_path(rt, preset, spp):
     dev = rt.DeviceScene(scene, 0)
     try:
         gpu, gs = dev.render(cam, st, fc, w, h)
+        rs = None
+        if preset == "c3":         # the reference's own TraversalStats units (rt_scene_config::traversal_ref)
+            with dev.configured(traversal_ref=1):
+                rgpu, rs = dev.render(cam, st, fc, w, h)
     finally:
         dev.close()
     assert gs.splat_mode == rt.abi.RT_SPLAT_STREAM
@@ -74,6 +78,26 @@ def test_full_frame_default_path(rt, preset, spp):
     assert np.isfinite(gpu).all() and np.isfinite(cpu).all()
     assert err <= 1e-5
     check_traversal(gs, walk.result)
+    if rs is not None:
+        ref_report = check_traversal_ref(rs, cs)
+        REPORT[f"fullscale_{preset}_1080p_{spp}spp"]["traversal_ref_units"] = ref_report
+        assert (rs.closest_hit_rays, rs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
+        assert rel_l2(rgpu, cpu) <= 1e-5
+
+
+def check_traversal_ref(rs, cs, tol=1e-3):
+    """rt_stats::traversal_ref (the GPU walk counting the reference's units, RT/intersection.cpp:254,
+    :274-380) against the reference's own counts of the same frame (the oracle's reference walk):
+    within `tol` per field and query kind.  Returns the report."""
+    out = {}
+    for k, kind in enumerate(("closest", "shadow")):
+        g, r = rs.traversal_ref[k].as_dict(), cs.traversal[k].as_dict()
+        out[kind] = {"gpu_ref_units": g, "reference_walk": r,
+                     "rel_diff": {f: (g[f] - r[f]) / max(r[f], 1) for f in g}}
+    for kind in ("closest", "shadow"):
+        for f, d in out[kind]["rel_diff"].items():
+            assert abs(d) <= tol, (kind, f, out[kind])
+    return out
 
 
 def traversal_report(gs, cs, walk):
