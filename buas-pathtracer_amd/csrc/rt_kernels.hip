@@ -1749,11 +1749,22 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_
 // k_trace<true>  — intersect_shadow_ray for every queued shadow ray (:600-604,
 //                  RT/integrators.cpp:756); unoccluded NEE contributions are
 //                  added to the path's total_color.
-// Persistent waves: each wave grabs CHUNK queue items with one atomic and
+// Persistent waves: each wave grabs CHUNK_EXT / CHUNK_SH queue items with one atomic and
 // refills lanes whose query has finished from that chunk (Aila & Laine 2009,
 // for 64-wide waves), so lanes do not idle behind the wave's longest ray.
 constexpr int TB = 256;                     // threads per persistent trace block
-constexpr uint32_t CHUNK = 256;             // queue items a wave takes per fetch
+constexpr uint32_t CHUNK = 256;             // queue items a wave takes per fetch (k_drain)
+// k_trace<false> / k_trace<true>: 128 (r05).  Only ~13 % of the closest and ~5 % of the shadow rays enter a
+// BVH, so a launch has ~1 chunk of 256 per wave and its end waits on the waves holding the last ones; 128
+// gives a rank's share of 8 +3.5 %, the full C3 / C4 frames within +-0.3 %; 96 or a chunk sized per launch
+// for 2-3 fetches per wave less (profiles/r05_chunk_ab.txt).
+#ifndef RT_CHUNK_EXT
+#define RT_CHUNK_EXT 128
+#endif
+#ifndef RT_CHUNK_SH
+#define RT_CHUNK_SH 128
+#endif
+constexpr uint32_t CHUNK_EXT = RT_CHUNK_EXT, CHUNK_SH = RT_CHUNK_SH;
 constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 
 // VGPR budget.  The block's LDS (a 16-entry stack + the hit barycentrics, 34.8 KB) allows 4
@@ -1784,6 +1795,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     __shared__ uint32_t qlen[NSHARD];
     if (threadIdx.x < NSHARD) qlen[threadIdx.x] = OCC ? cnt->shadow_count[threadIdx.x][0] : cnt->ext_count[cur][threadIdx.x][0];
     __syncthreads();
+    constexpr uint32_t chunk = OCC ? CHUNK_SH : CHUNK_EXT;
     // a wave drains its own shard first, then the others (a plain read of a head
     // skips exhausted shards without an atomic)
     uint32_t shard = blockIdx.x % NSHARD, tried = 0;
@@ -1823,11 +1835,11 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
                     uint32_t base = 0xFFFFFFFFu;
                     if (lane == (uint32_t)leader &&
                         __hip_atomic_load(head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < len)
-                        base = atomicAdd(head, CHUNK);
+                        base = atomicAdd(head, chunk);
                     base = (uint32_t)__builtin_amdgcn_readlane((int)base, leader);   // wave-uniform: SGPRs
                     if (base < len) {
                         chunk_next = shard*pool.shard_cap + base;
-                        chunk_end = shard*pool.shard_cap + min(base + CHUNK, len);
+                        chunk_end = shard*pool.shard_cap + min(base + chunk, len);
                         got = true;
                         break;
                     }
