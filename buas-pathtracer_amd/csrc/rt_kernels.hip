@@ -1514,7 +1514,10 @@ RT_D uint32_t tile_of(const FrameParams& fp, uint32_t x, uint32_t y) { return di
 // Kernels
 // ======================================================================
 constexpr int BLOCK = 256;      // slot-ordered kernels (generate / shade)
-constexpr int EV_SLOTS = 8;     // iterations in flight per partition in run_frame (2 chunks of 4)
+// chunks in flight per partition in run_frame: 3 or 4 lose (the empty chunks after a partition's end
+// cost more than the early chunks' host round trips: profiles/r05_host_ab.txt)
+constexpr int NIF = 2;
+constexpr int EV_SLOTS = 4*NIF;  // iterations in flight per partition in run_frame (NIF chunks of 4)
 
 // The splat of a finished path (RT/raytracer.cpp:469-488): vignette (L . vig), then the
 // 20-byte sample record k_resolve gathers (splat_filter :187-259 in reference order), or
@@ -1758,13 +1761,7 @@ constexpr uint32_t CHUNK = 256;             // queue items a wave takes per fetc
 // BVH, so a launch has ~1 chunk of 256 per wave and its end waits on the waves holding the last ones; 128
 // gives a rank's share of 8 +3.5 %, the full C3 / C4 frames within +-0.3 %; 96 or a chunk sized per launch
 // for 2-3 fetches per wave less (profiles/r05_chunk_ab.txt).
-#ifndef RT_CHUNK_EXT
-#define RT_CHUNK_EXT 128
-#endif
-#ifndef RT_CHUNK_SH
-#define RT_CHUNK_SH 128
-#endif
-constexpr uint32_t CHUNK_EXT = RT_CHUNK_EXT, CHUNK_SH = RT_CHUNK_SH;
+constexpr uint32_t CHUNK_EXT = 128, CHUNK_SH = 128;
 constexpr int STEPS_PER_REFILL = 8;         // trace steps between lane refills
 
 // VGPR budget.  The block's LDS (a 16-entry stack + the hit barycentrics, 34.8 KB) allows 4
@@ -3028,8 +3025,8 @@ struct Partition {
     Pool pool = {};
     std::vector<void*> pool_allocs;
     Counters* cnt = nullptr;
-    Counters* cnt_host = nullptr;       // pinned, [3]: the counters after chunk c land in [c % 2]; [2] stages the frame's initial counters
-    hipEvent_t chunk_done[2] = {};
+    Counters* cnt_host = nullptr;       // pinned, [NIF + 1]: the counters after chunk c land in [c % NIF]; [NIF] stages the frame's initial counters
+    hipEvent_t chunk_done[NIF] = {};
     uint2* spill = nullptr;             // traversal stack levels beyond STACK_LDS
     hipStream_t own_stream = nullptr;   // partitions > 0 (partition 0 runs on the caller's stream)
     hipEvent_t join = nullptr;
@@ -3250,7 +3247,7 @@ int ensure_partition(rt_scene* s, int k) {
     Partition& pt = s->part[k];
     if (pt.cnt) return RT_OK;
     HIP_OK(hipMalloc(&pt.cnt, sizeof(Counters)));
-    HIP_OK(hipHostMalloc(&pt.cnt_host, 3*sizeof(Counters)));
+    HIP_OK(hipHostMalloc(&pt.cnt_host, (NIF + 1)*sizeof(Counters)));
     for (auto& e : pt.chunk_done) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_OK(hipMalloc(&pt.spill, sizeof(uint2)*(size_t)(STACK_DEPTH - std::min(STACK_LDS, TRACE_STACK_LDS))*s->trace_grid*TB));
     if (k > 0) HIP_OK(hipStreamCreateWithFlags(&pt.own_stream, hipStreamNonBlocking));
@@ -3422,7 +3419,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     HIP_OK(hipEventRecord(s->start_ev, stream));
     struct Run { hipStream_t stream; uint32_t grid; uint64_t iters, chunks, consumed; int cur; bool live, drain, near;
                  unsigned long long seen_next; int final_buf;
-                 uint64_t chunk_first[2]; int chunk_n[2]; uint32_t pass0, pass1, ring; float4* dst;
+                 uint64_t chunk_first[NIF]; int chunk_n[NIF]; uint32_t pass0, pass1, ring; float4* dst;
                  bool res_ev[EV_SLOTS]; };
     Run run[MAX_PARTITIONS] = {};
     double kms[RT_KERNEL_COUNT] = {};
@@ -3476,8 +3473,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         }
         init.start_sample = init.next_sample;
         r.seen_next = init.next_sample;
-        pt.cnt_host[2] = init;           // pinned: the copy is asynchronous (the frame ends before the next write)
-        HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + 2, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
+        pt.cnt_host[NIF] = init;         // pinned: the copy is asynchronous (the frame ends before the next write)
+        HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + NIF, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
         HIP_OK(hipMemsetAsync(pt.pool.fin_w, 0, 4ull*N / 64, r.stream));
@@ -3583,12 +3580,12 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     };
     // A chunk: 4 iterations (1 in a partition's first 3 chunks), then the counters into
     // the pinned buffer of the chunk's parity and an event.  Every live partition keeps
-    // two chunks in flight, so while the host reads one chunk's counters the next one
+    // NIF = two chunks in flight, so while the host reads one chunk's counters the next one
     // already runs and the partitions never drain between host checks.
     auto enqueue_chunk = [&](int k) -> int {
         Partition& pt = s->part[k];
         Run& r = run[k];
-        const int b = (int)(r.chunks & 1);
+        const int b = (int)(r.chunks % NIF);
         r.chunk_first[b] = r.iters;
         r.chunk_n[b] = r.chunks < 3 ? 1 : 4;
         for (int i = 0; i < r.chunk_n[b]; ++i) iterate(k, i == r.chunk_n[b] - 1);
@@ -3613,7 +3610,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     };
     s->cancel = 0;
     const double t_setup = debug_timing() ? host_ms() : 0.0;
-    for (int c = 0; c < 2; ++c)
+    for (int c = 0; c < NIF; ++c)
         for (int k = 0; k < nparts; ++k) {
             int err = enqueue_chunk(k);
             if (err) return err;
@@ -3622,19 +3619,27 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         fprintf(stderr, "[rt timing] run_frame: partitions set up %.3f ms, first chunks enqueued %.3f ms\n",
                 t_setup - std::chrono::duration<double, std::milli>(t0.time_since_epoch()).count(), host_ms() - t_setup);
     uint64_t rounds = 0;
+    std::string host_log;                        // RT_DEBUG_TIMING: the host's waits and enqueues
     for (int live = nparts; live > 0; ++rounds) {
         for (int k = 0; k < nparts; ++k) {
             Run& r = run[k];
             if (!r.live) continue;
-            const int b = (int)(r.consumed & 1);
+            const int b = (int)(r.consumed % NIF);
+            const double tw0 = debug_timing() ? host_ms() : 0.0;
             HIP_OK(hipEventSynchronize(s->part[k].chunk_done[b]));
+            if (debug_timing()) {
+                char buf[96];
+                snprintf(buf, sizeof buf, " p%d:c%llu@%.3f+%.3f", k, (unsigned long long)r.consumed,
+                         tw0 - t_setup, host_ms() - tw0);
+                host_log += buf;
+            }
             harvest(k, b);
             ++r.consumed;
             const Counters& c = s->part[k].cnt_host[b];
             if (c.next_sample >= c.total_samples) r.drain = true;     // the chunks enqueued from now on
             // the claims of a few more chunks reach the end: from now on the iterations carry the
             // fused-drain kernels (two chunks are in flight when the host sees a chunk's counters)
-            if (c.next_sample + 2*(c.next_sample - r.seen_next) >= c.total_samples) r.near = true;
+            if (c.next_sample + NIF*(c.next_sample - r.seen_next) >= c.total_samples) r.near = true;
             r.seen_next = c.next_sample;
             if (c.next_sample >= c.total_samples && c.pending == 0 && c.pending_splat == 0) {
                 r.live = false; r.final_buf = b; --live;       // its chunk still in flight finds nothing to do
@@ -3644,6 +3649,11 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
                 int err = enqueue_chunk(k);
                 if (err) return err;
             }
+        }
+        if (debug_timing()) {
+            char buf[48];
+            snprintf(buf, sizeof buf, " |%.3f\n", host_ms() - t_setup);
+            host_log += buf;
         }
         if (s->cancel || rounds > 1000000) {
             // Every partition may still have two chunks in flight that write the pool, the sample
@@ -3655,6 +3665,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             return RT_ERROR_DEVICE;
         }
     }
+    if (debug_timing()) fprintf(stderr, "[rt timing] host rounds (partition:chunk@wait start+wait ms | round end):\n%s", host_log.c_str());
     for (int k = 1; k < nparts; ++k) {                     // the caller's stream continues after every partition
         HIP_OK(hipEventRecord(s->part[k].join, run[k].stream));
         HIP_OK(hipStreamWaitEvent(stream, s->part[k].join, 0));
