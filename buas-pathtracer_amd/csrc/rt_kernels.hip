@@ -1237,13 +1237,13 @@ struct Pool {
     float4*   sh_c;      // [N] contribution.xyz
     uint32_t* sh_dst;    // [N] the NEE term's destination (survivor's nx slot or SH_FIN | entry)
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
-    uint32_t* free_n;    // [blocks]: the block's slots past its survivors, for the next k_generate (k_shade)
-    uint32_t* claim_base;// [blocks]: exclusive scan of free_n (k_bookkeep) = first claim of the block
+    uint32_t* claim_base;// [blocks]: exclusive scan of the blocks' free slots (k_bookkeep: block_free) = first
+                         // claim of the block
     PathOut nx;          // the other buffer: k_shade's survivors, k_connect's NEE terms for them
     // finished paths, per wave of 64 slots compacted from the wave's first entry (k_shade; the next
     // k_generate splats them, k_connect adds a pending last NEE term): {L, vignette}, {ray_d.w key,
     // tile-list pixel p}, ray_o.w pixel; fin_w[wave] of them.  free_w[wave]: the wave's slots past
-    // its survivors (free_n[block] is their sum).  The AA jitter is recomputed (sample_jitter).
+    // its survivors (block_free sums a block's four).  The AA jitter is recomputed (sample_jitter).
     float4*   fin_L;
     uint2*    fin_k;
     uint32_t* fin_px;
@@ -1266,6 +1266,7 @@ enum : uint8_t { S_FREE = 0, S_TRACE = 1, S_DONE = 2, S_NEW = 3 };
 // the bounce-0 flags), and k_shade / k_drain make them from the state, the vignette from the camera
 // ray (new_path_records); 32 B per new path less to write.
 constexpr int REC_Q = 3;     // float4 per queued ray record
+
 constexpr uint32_t SH_FIN = 0x80000000u;   // Pool::sh_slot: the shadow ray's path is in the finished array
 
 // Queues and fetch heads are sharded NSHARD ways (shard = blockIdx % NSHARD, the
@@ -1406,7 +1407,7 @@ RT_D void block_count(uint32_t* counter, bool pred, uint32_t* scratch) {
     if (threadIdx.x == 0 && total) atomicAdd(counter, total);
 }
 
-// K block-wide tallies at once (the end of k_generate / k_shade): one ballot per
+// K block-wide tallies at once (k_drain_list; k_generate / k_shade until r05): one ballot per
 // predicate, ONE barrier to publish the per-wave counts, then thread 0 scans the
 // waves and adds each tally's block total to ctr[k] (a null ctr: total only), all K
 // atomics in flight together; one barrier to publish the bases.  The
@@ -1721,32 +1722,25 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_
             enqueue = pro.bvh;
         }
     }
-    // new paths that enter the BVH go to the current extension queue behind the survivors
+    // new paths that enter the BVH go to the current extension queue: one returning atomic per wave,
+    // no barrier (r05, as in k_shade's tail)
     const uint32_t shard = blockIdx.x % NSHARD;
-    __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
-    __shared__ uint32_t wcalls[BLOCK / 64];         // the camera rays' mesh instances reached (rt_stats::traversal)
-    {
-        const uint32_t wsum = __ockl_wfred_add_u32(pro.calls);
-        if (lane == 0) wcalls[wave] = wsum;
-    }
-    const bool tp[1] = {enqueue};
-    uint32_t* const tc[1] = {&cnt->ext_count[cur][shard][0]};
-    uint32_t tpos[1], ttot[1];
-    block_tally<BLOCK, 1>(tp, tc, tpos, ttot, tally);
-    if (threadIdx.x == 0) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int w = 0; w < BLOCK / 64; ++w) c += wcalls[w];
-        if (c) atomicAdd(&cnt->trav[shard][TV_CALLS], (unsigned long long)c);
-    }
-    const uint32_t pos = tpos[0];
+    const unsigned long long emask = __ballot(enqueue);
+    const uint32_t wsum = __ockl_wfred_add_u32(pro.calls);
+    uint32_t got = 0;
+    if (lane == 0 && emask) got = atomicAdd(&cnt->ext_count[cur][shard][0], (uint32_t)__popcll(emask));
+    if (lane == 1 && wsum) __hip_atomic_fetch_add(&cnt->trav[shard][TV_CALLS], (unsigned long long)wsum, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ebase = (uint32_t)__builtin_amdgcn_readlane((int)got, 0);
     if (enqueue) {
-        float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + pos);
+        float4* q = pool.ext_rec[cur] + REC_Q*((size_t)shard*pool.shard_cap + ebase +
+                                               (uint32_t)__popcll(emask & ((1ull << lane) - 1ull)));
         q[0] = make_float4(nro.x, nro.y, nro.z, __uint_as_float(slot));
         q[1] = make_float4(nrd.x, nrd.y, nrd.z, pro.t);
         q[2] = make_float4(pro.inv_d.x, pro.inv_d.y, pro.inv_d.z, __uint_as_float(pro.mlist));
     }
 }
+
 
 // k_trace<false> — intersect_scene for every queued path (RT/intersection.cpp:606-610)
 // k_trace<true>  — intersect_shadow_ray for every queued shadow ray (:600-604,
@@ -2220,42 +2214,51 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         pool.free_w[slot >> 6] = 64u - (uint32_t)__popcll(cmask);
         pool.fin_w[slot >> 6] = (uint32_t)__popcll(fmask);
     }
-    __shared__ uint32_t tally[(BLOCK / 64 + 2)*6];
-    // the wave's mesh instances reached by its prologues (rt_stats::traversal), next bounce | shadow << 16
-    // (at most 64 x 63 each); published before the tally's first barrier, added up after it
-    __shared__ uint32_t wcalls[BLOCK / 64];
+    // Each wave appends to its shard's queues with its own returning atomic (lanes 0 and 1: extension,
+    // shadow; one instruction) and adds the other counters with no-return atomics: no barrier, so a wave
+    // leaves without waiting for its block's slowest one (r05; the block tally's two barriers and its
+    // thread-0 atomics before: C4 +2.2 % in five A/B pairs, C3 and a rank's share of 8 within +-0.4 %,
+    // profiles/r05_wave_append_ab.txt).  Four times the atomics on a shard's queue counter (~16k per
+    // launch at C3's pool) stay under the ~88 per us one word sustains.  k_bookkeep sums free_w.
     {
+        const unsigned long long emask = __ballot(enq), smask = __ballot(shadow), xmask = __ballot(cast_shadow);
+        const uint32_t lane = __lane_id();
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        uint32_t* ap = nullptr;
+        uint32_t av = 0;
+        if (lane == 0) { ap = &cnt->ext_count[nxt][shard][0]; av = (uint32_t)__popcll(emask); }
+        if (lane == 1) { ap = &cnt->shadow_count[shard][0]; av = (uint32_t)__popcll(smask); }
+        uint32_t got = 0;
+        if (av) got = atomicAdd(ap, av);
+        // the other counters, no-return: alive, shadow rays cast, finished; the mesh instances reached
+        uint32_t* np = nullptr;
+        uint32_t nv = 0;
+        if (lane == 2) { np = &cnt->alive[shard][0]; nv = (uint32_t)__popcll(cmask); }
+        if (lane == 3) { np = &cnt->cast[1][shard][0]; nv = (uint32_t)__popcll(xmask); }
+        if (lane == 4) { np = &cnt->unsplat[shard][0]; nv = (uint32_t)__popcll(fmask); }
+        if (nv) __hip_atomic_fetch_add(np, nv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t c = cpro.calls | ((cast_shadow ? (uint32_t)sh_calls[threadIdx.x] : 0u) << 16);
         const uint32_t wsum = __ockl_wfred_add_u32(c);
-        if (__lane_id() == 0) wcalls[threadIdx.x >> 6] = wsum;
+        unsigned long long* cp = nullptr;
+        uint32_t cv = 0;
+        if (lane == 5) { cp = &cnt->trav[shard][TV_CALLS]; cv = wsum & 0xFFFFu; }
+        if (lane == 6) { cp = &cnt->trav[shard][TV_N + TV_CALLS]; cv = wsum >> 16; }
+        if (cv) __hip_atomic_fetch_add(cp, (unsigned long long)cv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t ebase = (uint32_t)__builtin_amdgcn_readlane((int)got, 0);
+        const uint32_t sbase = (uint32_t)__builtin_amdgcn_readlane((int)got, 1);
+        if (enq) {
+            float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + ebase + (uint32_t)__popcll(emask & lt));
+            stnt(&q[0], make_float4(nro.x, nro.y, nro.z, __uint_as_float(nslot)));
+            stnt(&q[1], make_float4(nrd.x, nrd.y, nrd.z, cpro.t));
+            stnt(&q[2], make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, __uint_as_float(cpro.mlist)));
+        }
+        if (shadow) {
+            pool.sh_slot[(size_t)shard*pool.shard_cap + sbase + (uint32_t)__popcll(smask & lt)] = slot;
+            pool.sh_dst[slot] = cont ? nslot : (SH_FIN | fidx);
+        }
     }
-    const bool tp[6] = {enq, shadow, cont, cast_shadow, fin, slot < pool.n && !cont};
-    uint32_t* const tc[6] = {&cnt->ext_count[nxt][shard][0], &cnt->shadow_count[shard][0], &cnt->alive[shard][0],
-                             &cnt->cast[1][shard][0], &cnt->unsplat[shard][0], nullptr};
-    uint32_t tpos[6], ttot[6];
-    block_tally<BLOCK, 6>(tp, tc, tpos, ttot, tally);
-    if (threadIdx.x == 0) {
-        uint32_t c0 = 0, c1 = 0;
-#pragma unroll
-        for (int w = 0; w < BLOCK / 64; ++w) { c0 += wcalls[w] & 0xFFFFu; c1 += wcalls[w] >> 16; }
-        if (c0) atomicAdd(&cnt->trav[shard][TV_CALLS], (unsigned long long)c0);
-        if (c1) atomicAdd(&cnt->trav[shard][TV_N + TV_CALLS], (unsigned long long)c1);
-    }
-    const uint32_t pos = tpos[0];
-    if (enq) {
-        float4* q = pool.ext_rec[nxt] + REC_Q*((size_t)shard*pool.shard_cap + pos);
-        stnt(&q[0], make_float4(nro.x, nro.y, nro.z, __uint_as_float(nslot)));
-        stnt(&q[1], make_float4(nrd.x, nrd.y, nrd.z, cpro.t));
-        stnt(&q[2], make_float4(cpro.inv_d.x, cpro.inv_d.y, cpro.inv_d.z, __uint_as_float(cpro.mlist)));
-    }
-    const uint32_t spos = shard*pool.shard_cap + tpos[1];
-    if (shadow) {
-        // the NEE term goes to the survivor's L in pool.nx, or to the finished entry
-        pool.sh_slot[spos] = slot;
-        pool.sh_dst[slot] = cont ? nslot : (SH_FIN | fidx);
-    }
-    if (threadIdx.x == 0) pool.free_n[blockIdx.x] = ttot[5];
 }
+
 
 
 // The frame's drain, fused.  Once nothing is left to claim and few paths are alive, an iteration
@@ -2755,6 +2758,12 @@ struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0; };
 // -1.0 % (profiles/r04_bookkeep_ab.txt).
 constexpr int BK_THREADS_SMALL = 1024, BK_THREADS_LARGE = 512;
 constexpr uint32_t BK_LARGE_POOL = 4u << 20;
+// A k_shade block's slots past its survivors: its four waves' free_w in one 16-byte load.
+static_assert(BLOCK == 256, "block_free: a k_shade block is four waves");
+RT_D uint32_t block_free(const Pool& pool, uint32_t b) {
+    const uint4 f = reinterpret_cast<const uint4*>(pool.free_w)[b];
+    return f.x + f.y + f.z + f.w;
+}
 template <int BK_THREADS>
 __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool pool, uint32_t nblocks, int cur, int phase,
                                                          ResPlan plan) {
@@ -2778,7 +2787,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
     uint32_t v[BK_EMAX];
     if (E <= BK_EMAX) {
 #pragma unroll
-        for (uint32_t j = 0; j < BK_EMAX; ++j) v[j] = lo + j < hi ? pool.free_n[lo + j] : 0u;
+        for (uint32_t j = 0; j < BK_EMAX; ++j) v[j] = lo + j < hi ? block_free(pool, lo + j) : 0u;
     }
     __shared__ uint32_t skip;
     if (t < 64) {
@@ -2870,7 +2879,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
     }
     __syncthreads();
     if (skip) return;
-    // exclusive scan of free_n: thread t owns the contiguous entries [t*E, t*E + E), sums them,
+    // exclusive scan of the free counts: thread t owns the contiguous entries [t*E, t*E + E), sums them,
     // then a wave scan by shuffles and one barrier for the 16 wave totals.
     // (A Hillis-Steele scan over 1024 threads took 20 barriers per 4096 entries: the single
     // workgroup ran 26 us alone and ~200 us beside the other partitions' kernels.)
@@ -2879,7 +2888,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
 #pragma unroll
         for (uint32_t j = 0; j < BK_EMAX; ++j) sum += v[j];
     } else {
-        for (uint32_t i = lo; i < hi; ++i) sum += pool.free_n[i];
+        for (uint32_t i = lo; i < hi; ++i) sum += block_free(pool, i);
     }
     const uint32_t lane = t & 63u, wave = t >> 6;
     uint32_t incl = sum;
@@ -2899,7 +2908,7 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             if (lo + j < hi) { pool.claim_base[lo + j] = run; run += v[j]; }
     } else {
         for (uint32_t i = lo; i < hi; ++i) {
-            const uint32_t x = pool.free_n[i];
+            const uint32_t x = block_free(pool, i);
             pool.claim_base[i] = run;
             run += x;
         }
@@ -3270,7 +3279,6 @@ int ensure_pool(Partition& pt, uint32_t n) {
     const size_t cap = (nblocks + NSHARD - 1) / NSHARD * BLOCK;   // a block appends <= BLOCK entries per queue
     const size_t Q = cap*NSHARD;
     p.shard_cap = (uint32_t)cap;
-    e |= alloc((void**)&p.free_n, 4*nblocks);
     e |= alloc((void**)&p.claim_base, 4*nblocks);
     e |= alloc((void**)&p.fin_w, 4*(N / 64));
     e |= alloc((void**)&p.free_w, 4*(N / 64));
@@ -3476,7 +3484,6 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         pt.cnt_host[NIF] = init;         // pinned: the copy is asynchronous (the frame ends before the next write)
         HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + NIF, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
-        HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_n, BLOCK, r.grid, r.stream));   // N is a multiple of BLOCK
         HIP_OK(hipMemsetAsync(pt.pool.fin_w, 0, 4ull*N / 64, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_w, 64, N / 64, r.stream));
         launch_bookkeep(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{}, r.stream);
