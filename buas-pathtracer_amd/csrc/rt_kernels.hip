@@ -4244,6 +4244,10 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
             if ((err = upload(s, q.data(), q.size(), &ds.blob))) return fail(err);
             ds.blob_q = (uint32_t)q.size();
         }
+        if (debug_timing())
+            fprintf(stderr, "[rt timing] rt_scene_upload: scene tables %zu B (%s LDS; materials %zu, primitives %u, planes %u, "
+                    "transforms %zu, lights %u, meshes %zu)\n", blob.size(), ds.blob_q ? "in" : "not in", mats.size(),
+                    d->primitive_count, d->plane_count, inv.size(), d->light_count, meshes.size());
     }
     {
         hipDeviceProp_t prop;
