@@ -241,7 +241,11 @@ def main():
         def step(timing=None):
             accum.zero_()
             if args.shard_of > 1:                          # diagnostic: one rank's share of an N-rank frame
-                return render_shard(args.shard_index, args.shard_of, accum)
+                t0 = time.perf_counter()
+                s = render_shard(args.shard_index, args.shard_of, accum)
+                if timing is not None:
+                    timing.setdefault("render_s", []).append(time.perf_counter() - t0)
+                return s
             # this rank's share into a zeroed frame buffer, the RCCL sum-reduce of it over xGMI into
             # rank 0, which adds it to its accumulation buffer
             return render_frame_sharded(render_shard, accum, rank, world, scratch=scratch, reduce=distributed,
@@ -312,8 +316,8 @@ def main():
     # Per-rank diagnostics (N > 1): each rank's frame (render) times, its framebuffer reduce times and
     # its samples, gathered to rank 0 -- so a scaling shortfall reads as imbalance, tail or reduce.
     ranks_info = None
-    if distributed:
-        tsum = timing_summary(timing)
+    tsum = timing_summary(timing)
+    if distributed and tsum["render_ms"]:
         fr, rd = tsum["render_ms"], tsum["reduce_ms"]
         row = [min(fr), sum(fr) / len(fr), max(fr), (sum(rd) / len(rd)) if rd else 0.0, max(rd) if rd else 0.0,
                float(samples), 1e3 * elapsed / args.steps]

@@ -176,7 +176,8 @@ class SceneConfig(C.Structure):       # rt_scene_config (per-scene schedule and 
                 ("partitions", C.c_int32), ("path_pool", C.c_int64), ("fuse_paths", C.c_int64),
                 ("splat_chunk", C.c_int32), ("splat_ring", C.c_int32), ("sample_budget_gb", C.c_double),
                 ("resolve_tall_pixels", C.c_int64), ("debug_traversal", C.c_int32), ("traversal_ref", C.c_int32),
-                ("reserved", C.c_int32 * 6)]
+                ("drain_every", C.c_int32),                 # ABI 8
+                ("reserved", C.c_int32 * 5)]
 
 
 class BvhInfo(C.Structure):

@@ -1621,8 +1621,9 @@ RT_D V2 sample_jitter(const DevScene& sc, const rt_settings& st, const FramePara
 // of 8 +1.4 %, C3 / C4 +0.1 / +0.2 % (profiles/r04_sgpr_ab.txt)
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                         Counters* cnt, int cur) {
-    // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
-    // splat them.  Their NEE contributions from k_connect are in by now.
+    // Once the partition is complete nothing is left to splat or claim (k_bookkeep sets done only
+    // when the last k_shade finished no path and continued none; the fused drain splats its own)
+    if (cnt->done) return;                          // uniform
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const uint32_t lane = __lane_id(), wave = (slot >> 6) & (uint32_t)(BLOCK / 64 - 1);   // wave in the group
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
@@ -2069,6 +2070,7 @@ template <bool IN_LDS, bool ENV>
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur, int sparse, int fuse) {
     if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
+    if (cnt->done) return;                          // the partition is complete (see k_drain_list)
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     // The slot's state and path record are loaded before the scene copy, whatever the
     // state: the three round trips (state, record, LDS blob) overlap instead of running
@@ -2086,7 +2088,6 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         h4 = ldnt(&pool.hit[slot]); r4 = ldnt(&pool.rng[slot]); hw = ldnt(&pool.hit_w[slot]);
     };
     if (sparse) {
-        if (cnt->done) return;                                          // uniform: every block reads it
         if (slot < pool.n) {
             state0 = pool.state[slot];
             if (state0 != S_FREE) load_path();
@@ -2220,6 +2221,9 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
     // thread-0 atomics before: C4 +2.2 % in five A/B pairs, C3 and a rank's share of 8 within +-0.4 %,
     // profiles/r05_wave_append_ab.txt).  Four times the atomics on a shard's queue counter (~16k per
     // launch at C3's pool) stay under the ~88 per us one word sustains.  k_bookkeep sums free_w.
+    // Invariant: every lane of the wave reaches this block.  The atomics are issued from fixed lanes
+    // (0..6) and the queue bases read back from lanes 0 and 1, so k_shade may only return where the
+    // whole wave does: the three returns above test Counters flags every lane reads alike.
     {
         const unsigned long long emask = __ballot(enq), smask = __ballot(shadow), xmask = __ballot(cast_shadow);
         const uint32_t lane = __lane_id();
@@ -2275,13 +2279,28 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
 //
 // k_drain_list (the fused iteration, after k_generate splatted the last finished array): the
 // survivors of the last k_shade (S_TRACE) go to Pool::sh_slot, sharded like the queues; the
-// finished arrays are emptied (their entries are splatted already).
+// finished arrays are emptied (their entries are splatted already), and the pool is retired:
+// every wave's free count goes to 64, so a k_generate launched after the drain marks every slot
+// of whichever buffer it gets S_FREE.
+//
+// Why the retirement (r06; the r05 every-4th-iteration carry lost the radiance of 13,120 samples
+// of one claim batch on C4-small).  k_drain leaves the pool states as they were, and free_w keeps
+// the counts of the k_shade before the drain.  The host enqueues iterations two chunks ahead; when
+// an iteration after the drain did not carry the drain kernels (fuse = 0), its k_shade was not held
+// back by Counters::fused: k_generate kept the first 64 - free_w slots of each wave of the other
+// buffer (the stale inputs of that k_shade, still S_TRACE), k_shade shaded them a second time, and
+// with k_bookkeep no longer resetting the counters once done, the connect and extend fetch heads
+// stood past the re-runs' new queue entries: shadow rays went untraced and mesh hits unfound, and
+// the re-runs splatted the poorer results over the finished records.  The default
+// schedule never ran into it only because every iteration after the first fused one carried the drain
+// kernels, whose fuse flag makes extend / shade / connect exit.  Now the drain leaves no live state
+// behind, and k_generate / k_shade exit once Counters::done is set, whatever the host's cadence.
 __global__ void __launch_bounds__(BLOCK) k_drain_list(Pool pool, Counters* cnt) {
     if (!cnt->fused || cnt->done) return;                              // uniform
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const uint8_t stv = slot < pool.n ? pool.state[slot] : S_FREE;
     const bool live = stv == S_TRACE || stv == S_NEW;
-    if (slot < pool.n && (slot & 63u) == 0) pool.fin_w[slot >> 6] = 0;
+    if (slot < pool.n && (slot & 63u) == 0) { pool.fin_w[slot >> 6] = 0; pool.free_w[slot >> 6] = 64; }
     const uint32_t shard = blockIdx.x % NSHARD;
     __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
     const bool tp[1] = {live};
@@ -3537,7 +3556,9 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         const int sparse = r.drain ? 1 : 0;
         // near the drain every iteration carries the fused-drain kernels; they run only in the
         // iteration after k_bookkeep set Counters::fused, whose extend / shade / connect then exit
-        const int fuse = (r.near && fuse_paths) ? 1 : 0;
+        // (rt_scene_config::drain_every > 1: only every Nth iteration, a test of cadence independence)
+        const uint32_t every = s->cfg.drain_every > 0 ? (uint32_t)s->cfg.drain_every : 1u;
+        const int fuse = (r.near && fuse_paths && r.iters % every == every - 1) ? 1 : 0;
         b(RT_KERNEL_GENERATE);
         k_generate<<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, r.cur);
         e(RT_KERNEL_GENERATE);
@@ -3859,6 +3880,7 @@ int check_config(const rt_scene_config* c) {
     else if (!(c->sample_budget_gb == c->sample_budget_gb)) bad = "sample_budget_gb";
     else if (c->resolve_tall_pixels < 0) bad = "resolve_tall_pixels";
     else if (c->traversal_ref != 0 && c->traversal_ref != 1) bad = "traversal_ref";
+    else if (c->drain_every < 0 || c->drain_every > 1024) bad = "drain_every (0..1024)";
     if (bad) { set_error(std::string("rt_scene_config: bad ") + bad); return RT_ERROR_INVALID; }
     return RT_OK;
 }
@@ -3904,6 +3926,7 @@ bool config_from_env(rt_scene_config& c) {
     if (num("RT_RES_TALL_PIXELS", 0, 1ll << 40, v)) c.resolve_tall_pixels = v;
     if (num("RT_DEBUG_TRAVERSAL", 0, 1, v)) c.debug_traversal = (int32_t)v;
     if (num("RT_TRAVERSAL_REF", 0, 1, v)) c.traversal_ref = (int32_t)v;
+    if (num("RT_DRAIN_EVERY", 0, 1024, v)) c.drain_every = (int32_t)v;
     return ok;
 }
 

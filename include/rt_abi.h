@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 /* ---------------------------------------------------------------- status */
 enum rt_status {
@@ -460,7 +460,7 @@ int rt_cancel(rt_scene* scene);
  * Two scenes in one process may differ.  rt_scene_upload starts a scene from
  * rt_scene_default_config(), then applies the test-override environment variables once
  * (RT_SPLAT, RT_PARTITIONS, RT_FUSE_PATHS, RT_SPLAT_CHUNK, RT_SPLAT_RING,
- * RT_SAMPLE_BUDGET_GB, RT_RES_TALL_PIXELS, RT_DEBUG_TRAVERSAL); nothing reads the
+ * RT_SAMPLE_BUDGET_GB, RT_RES_TALL_PIXELS, RT_DEBUG_TRAVERSAL, RT_DRAIN_EVERY); nothing reads the
  * environment per frame.  A field at RT_CONFIG_INHERIT follows the process-wide setter
  * above at each frame (rt_set_splat_mode / rt_set_shard_mode / rt_set_env_sampling /
  * rt_set_path_pool), so callers of those setters see no change. */
@@ -480,7 +480,10 @@ typedef struct rt_scene_config {
     int32_t  traversal_ref;         /* 1: also count rt_stats::traversal_ref (the reference's units);
                                        the trace kernels then walk the top level in the reference's
                                        order (slower: no prologue mesh lists) -- a diagnostic mode  */
-    int32_t  reserved[6];
+    int32_t  drain_every;           /* (ABI 8) fused-drain kernels ride on every Nth iteration once the
+                                       host expects the drain (N >= 1; 0 = auto: every iteration).  A
+                                       schedule knob for the tests: frames are identical for every N */
+    int32_t  reserved[5];
 } rt_scene_config;
 int rt_scene_default_config(rt_scene_config* out);
 int rt_scene_get_config(const rt_scene* scene, rt_scene_config* out);

@@ -93,4 +93,9 @@ def random_scene(rt, seed, w, h, spp=8, mesh_instances=70):
     st.caustics = int(rng.random() < 0.5)
     st.sampling_strategy = int(rng.choice([0, 1, 2]))
     fc = rt.load_reconstruction_kernel(str(rng.choice(["Mitchell Netravali", "Box", "Gaussian 3", "Lanczos 3"])))
+    # the reference's integrator switches (RT/raytracer.cpp:1974-1977): one of their 16 combinations
+    # (drawn last, so the scenes themselves do not change with it)
+    combo = int(rng.integers(0, 16))
+    for i, k in enumerate(("next_event_estimation", "importance_sample_lights", "use_mis", "importance_sample_diffuse")):
+        setattr(st, k, (combo >> i) & 1)
     return s, cam, st, fc

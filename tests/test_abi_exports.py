@@ -24,7 +24,7 @@ def test_every_declared_symbol_is_exported(rt):
     assert len(names) > 40
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.rt_abi_version() == 7
+    assert lib.rt_abi_version() == 8
 
 
 def test_ctypes_table_covers_header(rt):
@@ -84,4 +84,4 @@ def test_scene_config_defaults(rt):
     assert (c.splat_mode, c.shard_mode, c.env_sampling) == (a.RT_CONFIG_INHERIT,) * 3
     assert (c.partitions, c.path_pool, c.fuse_paths, c.splat_chunk, c.splat_ring) == (0, 0, -1, 0, 0)
     assert c.sample_budget_gb < 0 and c.resolve_tall_pixels == 0 and c.debug_traversal == 0
-    assert c.traversal_ref == 0
+    assert c.traversal_ref == 0 and c.drain_every == 0

@@ -426,6 +426,44 @@ def test_fused_drain_matches_separate_kernels(which, w, h, spp, request):
     assert out["all"][4] < out["off"][4]          # the fused drain ended the frame in fewer iterations
 
 
+@pytest.mark.parametrize("which", ["c3small", "c4small"])
+def test_fused_drain_any_cadence(which, request):
+    """Counters::fused is safe whatever iterations carry the drain kernels (rt_scene_config::
+    drain_every, r06).  With the drain kernels on only every 2nd ... 7th iteration, k_bookkeep sets
+    `fused` in iterations that run the separate extend / shade / connect launches, and iterations
+    without the drain kernels follow the drain.  r05's every-4th carry lost the radiance of one claim
+    batch on C4-small (82.6 % of pixels identical: stale pool slots re-shaded after the drain, see
+    k_drain_list).  Every cadence must give the default's exact-splat frame bit for bit (and so the
+    oracle's, test_frame_bitwise_vs_reference_order), the same ray counts, and the same per-sample
+    radiance through rt_trace_samples; also with the drain fused at once (every path alive)."""
+    rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
+    w, h = 192, 108
+    rng = np.random.default_rng(13)
+    xy, s = _sample_list(rng, w, h, 20000, st.samples_per_pixel)
+
+    def run(**cfg):
+        with dev.configured(splat_mode=rt.abi.RT_SPLAT_EXACT, **cfg):
+            fr, fs = dev.render(cam, st, fc, w, h)
+            samp, ss = dev.trace_samples(cam, st, w, h, xy, s)
+        rays = [(int(x.closest_hit_rays), int(x.shadow_rays), int(x.traced_rays[0]), int(x.traced_rays[1]))
+                for x in (fs, ss)]
+        return fr, samp, rays, int(fs.iterations)
+
+    ref = run()
+    report = {}
+    for every in (2, 3, 4, 7):
+        for fuse in (-1, 1000000000):
+            fr, samp, rays, iters = run(drain_every=every, fuse_paths=fuse)
+            same = float(np.all(fr == ref[0], axis=2).mean())
+            report[f"every{every}_fuse{'all' if fuse > 0 else 'auto'}"] = {
+                "pixels_identical": same, "samples_identical": bool(np.array_equal(samp, ref[1])),
+                "rays_equal": rays == ref[2], "iterations": [iters, ref[3]]}
+            assert rays == ref[2], (every, fuse)
+            assert np.array_equal(fr, ref[0]), (every, fuse, same)
+            assert np.array_equal(samp, ref[1]), (every, fuse)
+    REPORT[f"fused_drain_cadence_{which}"] = report
+
+
 @pytest.mark.parametrize("depth", [0, 1, 2])
 def test_fused_drain_shallow_paths(c1, depth):
     """max_bounce_count 0 (nothing traced: every path finished at generation), 1 and 2: the fused
