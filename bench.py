@@ -157,6 +157,36 @@ def cpu_baseline(rt, cfg, spp_override, seconds_budget=15.0):
                       f"nproc {hc['nproc']}), {dt:.1f} s, {rays} rays; again at {t125} threads"}
 
 
+def pmc_figures(tj, kname, bytes_per_unit, units_per_frame, launches_per_frame):
+    """The serialized (rocprofv3 --pmc) figures of kernel `kname` from one configuration's entry of
+    profiles/traffic.json, normalized per frame over the same frame as the algorithmic bytes: the sum
+    of the isolated durations and of the HBM bytes over ALL of the kernel's dispatches in one frame
+    (the early exits after a partition's end included) against bytes_per_unit x the units of one
+    frame.  `traffic` per launch divides the frame's counter bytes by the launches the units are
+    averaged over (the event-timed ones), so it is comparable with `achieved`.  None when the entry
+    is missing or was measured on a frame of another size (units per frame off by more than 10 %)."""
+    ent = (tj or {}).get("kernels", {}).get(kname)
+    frames = (tj or {}).get("frames_per_pass")
+    upf = ((tj or {}).get("units_per_frame") or {}).get(kname)
+    if not ent or not frames or not upf or not units_per_frame:
+        return None
+    if abs(upf / units_per_frame - 1.0) > 0.1:
+        return None
+    alg = bytes_per_unit * units_per_frame
+    disp = ent["dispatches"] / frames
+    iso_s = ent["isolated_mean_us"] * 1e-6 * disp
+    hbm = ent["hbm_bytes_per_launch"] * disp
+    gbs = alg / iso_s / 1e9
+    return {"isolated": {"frame_ms": round(iso_s * 1e3, 3), "dispatches_per_frame": round(disp, 1),
+                         "mean_dispatch_ms": round(ent["isolated_mean_us"] / 1e3, 4),
+                         "alg_bytes_per_frame": round(alg), "achieved": round(gbs, 1),
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "source": tj.get("source"),
+                         "normalization": "per frame: bytes_per_unit x units of one frame / the sum of the "
+                                          "kernel's serialized dispatch durations in one frame"},
+            "traffic": round(hbm / max(launches_per_frame, 1e-9)),
+            "traffic_per_frame": round(hbm), "traffic_ratio": round(hbm / alg, 3)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -209,6 +239,14 @@ def main():
     red_dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{device}"
 
     rt = import_package()
+
+    def traffic_cfg(name):
+        """profiles/traffic.json's entry for one bench configuration (tools/pmc_summary.py --traffic)."""
+        try:
+            with open(args.traffic_json) as f:
+                return json.load(f).get("configs", {}).get(name)
+        except (OSError, ValueError):
+            return None
     cfg = dict(CONFIGS[args.config])
     if args.width:
         cfg["w"] = args.width
@@ -351,20 +389,30 @@ def main():
     c4 = None
     if args.c4_steps > 0 and args.config != "c4" and args.shard_of <= 1:
         c4scene, c4dev, c4st, _, c4acc, c4step = setup("c4", CONFIGS["c4"]["w"], CONFIGS["c4"]["h"], asset_dir)
+        # C4's roofline is k_extend's (the kernel with the most GPU time there): HIP
+        # events around the extend launches only, in the warm-up and the timed frames
+        ext = STAGES.index("extend")
+        rt.lib().rt_set_profiling_stages(1 << ext)
         c4step()
         torch.cuda.synchronize(device)
         if distributed:
             dist.barrier()
         c0 = time.perf_counter()
         cr = [0, 0, 0]
+        cx = [0.0, 0, 0, 0]             # extend: event ms, launches, traced rays, trace steps
         for _ in range(args.c4_steps):
             cs = c4step()
             cr[0] += cs.closest_hit_rays
             cr[1] += cs.shadow_rays
             cr[2] += cs.samples
+            cx[0] += cs.kernel_ms[ext]
+            cx[1] += cs.kernel_launches[ext]
+            cx[2] += cs.traced_rays[0]
+            cx[3] += cs.trace_steps[0]
         torch.cuda.synchronize(device)
         if distributed:
             dist.barrier()
+        rt.lib().rt_set_profiling(0)
         ct = torch.tensor([time.perf_counter() - c0], dtype=torch.float64, device=red_dev)
         crt = torch.tensor(cr, dtype=torch.float64, device=red_dev)
         if distributed:
@@ -380,6 +428,28 @@ def main():
               "samples_per_s": round(float(crt[2]) / cel, 1),
               "samples_per_s_per_gpu": round(float(crt[2]) / cel / world, 1),
               "closest_hit_rays": int(crt[0]), "shadow_rays": int(crt[1])}
+        # rank 0's k_extend: 68 B per traced ray over the launches' HIP-event time;
+        # the serialized figures and counter traffic from profiles/traffic.json's c4 entry (same frame
+        # size only); the step fetches (128 B per trace step, the frames' own counts) against the L2 rate
+        if cx[1] and cx[0] > 0:
+            n = args.c4_steps
+            mean_s = cx[0] / cx[1] / 1e3
+            upl = cx[2] / cx[1]
+            gbs = BYTES_PER_UNIT["extend"] * upl / mean_s / 1e9
+            tgbs = 128.0 * cx[3] / cx[1] / mean_s / 1e9
+            pmc4 = pmc_figures(traffic_cfg("c4"), "k_extend", BYTES_PER_UNIT["extend"], cx[2] / n, cx[1] / n)
+            c4["roofline"] = {"bound": "hbm", "kernel": "k_extend", "bytes_per_unit": BYTES_PER_UNIT["extend"],
+                              "units_per_launch": round(upl, 1), "mean_launch_ms": round(mean_s * 1e3, 4),
+                              "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(gbs / HBM_PEAK_GBS, 6),
+                              "traffic": pmc4["traffic"] if pmc4 else None,
+                              "traffic_ratio": pmc4["traffic_ratio"] if pmc4 else None,
+                              "isolated": pmc4["isolated"] if pmc4 else None,
+                              "traversal": {"bytes_per_step": 128, "steps_per_ray": round(cx[3] / max(cx[2], 1), 3),
+                                            "achieved": round(tgbs, 1), "peak": L2_PEAK_GBS,
+                                            "frac": round(tgbs / L2_PEAK_GBS, 4)},
+                              "timing": "HIP events around rank 0's extend launches in the timed C4 frames "
+                                        "(four partitions share the GPU)"}
 
     if rank == 0:
         rays = closest_all + shadow_all
@@ -397,21 +467,10 @@ def main():
         units_per_launch = units[dom] / max(kl[di], 1)
         alg_bytes = BYTES_PER_UNIT[dom] * units_per_launch
         achieved = alg_bytes / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
-        traffic = isolated = None
-        try:
-            with open(args.traffic_json) as f:
-                tj = json.load(f).get("configs", {}).get(args.config, {})
-            ent = tj.get("kernels", {}).get(KERNEL[dom])
-            # measured on launches of the same size (units per launch within 10 %), else stale
-            same = ent and (not ent.get("units_per_launch") or
-                            abs(ent["units_per_launch"] / max(units_per_launch, 1.0) - 1.0) <= 0.1)
-            if ent and same:
-                traffic = ent["hbm_bytes_per_launch"]
-                iso_gbs = alg_bytes / (ent["isolated_mean_us"] * 1e-6) / 1e9
-                isolated = {"mean_launch_ms": round(ent["isolated_mean_us"] / 1e3, 4), "achieved": round(iso_gbs, 1),
-                            "frac": round(iso_gbs / HBM_PEAK_GBS, 4), "source": tj.get("source")}
-        except (OSError, ValueError, KeyError):
-            pass
+        pmc = pmc_figures(traffic_cfg(args.config), KERNEL[dom], BYTES_PER_UNIT[dom], units[dom] / args.steps,
+                          kl[di] / args.steps)
+        traffic = pmc["traffic"] if pmc else None
+        isolated = pmc["isolated"] if pmc else None
         # Traversal kernels are bound by dependent L2 / Infinity Cache fetches, not HBM: their second
         # figure is the bytes their steps fetch -- every step loads one 128-byte round per lane (a BVH4
         # node, two triangles or a leaf record) -- counted in the timed frames by the kernels themselves
@@ -486,6 +545,10 @@ def main():
             # the rays handed to the BVH traversal kernels (closest, shadow); the rest were settled by the
             # planes / top-level prologue where they were made
             "traced_rays": [int(traced_all), int(traced_sh_all)],
+            # rank 0's units of work per frame per kernel (tools/pmc_summary.py --traffic keeps them with
+            # the PMC figures, which bench.py uses only for frames of the same size)
+            "units_per_frame": {KERNEL[k]: round(units[k] / args.steps, 1) for k in ("generate", "extend", "shade",
+                                                                                      "connect")},
             "config": {"workload": f"{args.config}: {cfg['preset']} {w}x{h} {st.samples_per_pixel}spp "
                                    f"depth {st.max_bounce_count}" + (" env-sampling" if args.env_sampling else ""),
                        "width": w, "height": h,
@@ -501,6 +564,8 @@ def main():
                          "kernel": KERNEL[dom], "bytes_per_unit": BYTES_PER_UNIT[dom],
                          "units_per_launch": round(units_per_launch, 1),
                          "mean_launch_ms": round(mean_launch_s * 1e3, 4),
+                         "traffic_ratio": pmc["traffic_ratio"] if pmc else None,
+                         "traffic_per_frame": pmc["traffic_per_frame"] if pmc else None,
                          "concurrency": round(concurrency, 2), "isolated": isolated, "traversal": traversal,
                          "pipeline": {"bytes": pipe_bytes, "achieved": round(pipe_gbs, 1),
                                       "frac": round(pipe_gbs / HBM_PEAK_GBS, 4),

@@ -33,7 +33,7 @@ for grp in "${GROUPS_RUN[@]}"; do
     if [ $FILTER = 0 ] || grep -qw -- "$c" $OUT/counters_list.txt || grep -qw -- "$base" $OUT/counters_list.txt; then keep="$keep $c"; else echo "$c" >> $OUT/dropped.txt; fi
   done
   if [ -z "$keep" ]; then echo "pass $i [$grp]: no counter available"; continue; fi
-  timeout -s KILL 300 rocprofv3 --pmc $keep --output-format csv -d $ROOTDIR/$OUT/pass$i -o run -- python3 $ROOTDIR/bench.py ${PMC_BENCH:---steps 1 --warmup 0 --no-cpu-baseline} > $OUT/pass$i.log 2>&1
+  timeout -s KILL 300 rocprofv3 --pmc $keep --output-format csv -d $ROOTDIR/$OUT/pass$i -o run -- python3 $ROOTDIR/bench.py ${PMC_BENCH:---steps 1 --warmup 0 --no-cpu-baseline} --c4-steps 0 > $OUT/pass$i.log 2>&1
   rc=$?; echo "pass $i [$keep] rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done

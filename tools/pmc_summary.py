@@ -122,7 +122,14 @@ def main():
             for line in open(a.bench_log):
                 if line.startswith("{"):
                     b = json.loads(line)
+                    if b.get("c4"):
+                        raise SystemExit("the PMC bench run also rendered C4 frames (--c4-steps 0 needed): "
+                                         "its dispatch counts mix two configurations")
                     rec["bench_spp"] = b["config"].get("spp")
+                    # frames the PMC pass rendered, and rank 0's units per frame per kernel: bench.py
+                    # normalizes the counters per frame (pmc_figures) and uses them for frames of this size
+                    rec["frames_per_pass"] = b["steps"] + b["warmup"]
+                    rec["units_per_frame"] = b.get("units_per_frame")
                     # the units per launch of the dominant kernel in that run: bench.py uses the isolated
                     # time only for launches of the same size
                     rf = b.get("roofline") or {}

@@ -16,6 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--bucket-ms", type=float, default=5.0)
+    ap.add_argument("--gap-us", type=float, default=150.0)
     a = ap.parse_args()
     rows = [r for r in csv.DictReader(open(a.trace)) if r["Kernel_Name"].startswith(("k_", "void k_"))]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -49,6 +50,30 @@ def main():
     if res:
         r = res[-1]
         print(f"last resolve {(int(r['Start_Timestamp']) - t0) / 1e6:.1f} -> {(int(r['End_Timestamp']) - t0) / 1e6:.1f} ms")
+    # per queue (a partition's stream): idle gaps longer than --gap-us between one kernel's end and the
+    # next one's start, with the kernels on either side
+    qcol = next((c for c in ("Queue_Id", "Queue_ID", "Stream_Id") if c in fr[0]), None)
+    if qcol:
+        byq = {}
+        for r in fr:
+            byq.setdefault(r[qcol], []).append(r)
+        for q, rs in sorted(byq.items()):
+            rs.sort(key=lambda r: int(r["Start_Timestamp"]))
+            gaps = []
+            end = int(rs[0]["End_Timestamp"])
+            for prev, r in zip(rs, rs[1:]):
+                s = int(r["Start_Timestamp"])
+                if s - end > a.gap_us * 1e3:
+                    gaps.append(f"{(end - t0) / 1e6:.2f}->{(s - t0) / 1e6:.2f} ({(s - end) / 1e3:.0f} us, "
+                                f"{short(prev)} -> {short(r)})")
+                end = max(end, int(r["End_Timestamp"]))
+            print(f"queue {q}: {len(rs)} kernels, {(int(rs[0]['Start_Timestamp']) - t0) / 1e6:.2f}-"
+                  f"{(end - t0) / 1e6:.2f} ms, idle gaps: " + ("; ".join(gaps) or "none"))
+
+
+def short(r):
+    n = r["Kernel_Name"].split("(")[0].replace("void ", "")
+    return n.split("<")[0] + ("<" + n.split("<")[1].split(",")[0] + ">" if "k_trace" in n else "")
 
 if __name__ == "__main__":
     main()
