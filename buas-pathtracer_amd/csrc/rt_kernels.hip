@@ -857,7 +857,8 @@ struct Traversal {
                 co = ir.o; cd = ir.d; cinv = ir.inv_d;
                 // (reference units: no degenerate-axis pruning, so the walk visits the reference's nodes)
                 cflags = ir.neg | (REF ? 0u : ir.zero << 3) | ((sc.finite_boxes && finite_box_ray(ir.o, ir.inv_d)) ? 64u : 0u);
-                if (REF) { rp[0] = 1u; rp[1] = 0u; rp[2] = 0u; }    // the reference pops the root (:266-274)
+                // the reference pops the root (:266-274) of a mesh that has a BVH (:259; leaf record q5.w)
+                if (REF) { rp[0] = F[5].w != 0.0f ? 1u : 0u; rp[1] = 0u; rp[2] = 0u; }
                 inst = pi; node_off = __float_as_uint(F[3].z); tri_off = __float_as_uint(F[3].w);
                 if (!LST) mesh_base = sp;              // LST: the stack holds this mesh only
                 const V3 rp = {F[4].y, F[4].z, F[4].w}, rr = {F[5].x, F[5].y, F[5].z};
@@ -4164,7 +4165,11 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
                 const uint32_t root = root4[p.mesh_index];
                 q[3] = make_float4(u2f(pi), u2f(p.type), u2f(meshes[p.mesh_index].node_offset), u2f(meshes[p.mesh_index].tri_offset));
                 q[4] = make_float4(u2f(root), rn.bv_p.x, rn.bv_p.y, rn.bv_p.z);
-                q[5] = make_float4(rn.bv_r.x, rn.bv_r.y, rn.bv_r.z, 0.0f);
+                // q5.w: the mesh has a BVH.  Without one the reference tests none of its triangles
+                // (intersect_mesh, RT/intersection.cpp:259: `if (bvh)`): the root box is made empty
+                // (half sides -1: no slab test passes), and the reference-unit walk counts no root pop
+                if (M.node_count) q[5] = make_float4(rn.bv_r.x, rn.bv_r.y, rn.bv_r.z, 1.0f);
+                else q[5] = make_float4(-1.0f, -1.0f, -1.0f, 0.0f);
             } else {
                 bool translate = std::isfinite(iv.e[0][3]) && std::isfinite(iv.e[1][3]) && std::isfinite(iv.e[2][3]);
                 for (int r = 0; r < 3; ++r)

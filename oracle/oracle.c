@@ -554,6 +554,7 @@ static int intersect_mesh(const rt_mesh* mesh, const Ray* ray, int occlusion, fl
     uint32_t at = 0;
     uint64_t trav = 0, nodes = 0, leaves = 0, nodes4 = 0, tristeps = 0;
     if (ts) ts[TS_CALLS]++;
+    if (!mesh->node_count || !mesh->nodes) return 0;            /* `if (bvh)` (:259): no BVH, no triangle */
     stack[at++] = 0;
     while (at > 0) {
         const uint32_t e = stack[--at], odd = e >> 31;

@@ -142,3 +142,47 @@ def test_desc_keeps_its_scene_alive(rt):
     fc = rt.load_reconstruction_kernel("Box")
     frame, stats = ob.render(d, cam, st, fc, 8, 6, rng_mode=0, threads=1)
     assert stats.samples == 48 and np.isfinite(frame).all()
+
+
+class _DescOverride:
+    """A scene whose rt_scene_desc differs from its host scene's: mesh `m` without its BVH
+    (node_count 0), which rt_scene_upload accepts and the reference renders as a mesh whose
+    triangles are never tested (intersect_mesh counts the call, RT/intersection.cpp:254, then
+    skips everything under `if (bvh)`, :259)."""
+
+    def __init__(self, rt, scene, m):
+        self.scene = scene
+        d = scene.desc()
+        n = d.mesh_count
+        self._meshes = (rt.abi.Mesh * n)(*[d.meshes[i] for i in range(n)])
+        self._meshes[m].node_count = 0
+        self._meshes[m].nodes = None
+        self._desc = rt.abi.SceneDesc.from_buffer_copy(d)
+        self._desc.meshes = self._meshes
+
+    def desc(self):
+        return self._desc
+
+
+@pytest.mark.gpu
+def test_mesh_without_bvh(rt):
+    """a mesh uploaded without a BVH.  Frames and samples against the oracle as every
+    scene here (the mesh is invisible on both sides), the reference's TraversalStats units
+    (rt_scene_config::traversal_ref) against its own walk: the call is counted, no root pop."""
+    from parity_report import REPORT
+    from test_gpu_fullscale import check_traversal_ref
+    w, h = 96, 54
+    scene, cam, st, fc, post = rt.load_preset("c4", w, h)
+    st.samples_per_pixel = 8
+    sc = _DescOverride(rt, scene, 0)
+    _compare(rt, "mesh_without_bvh", sc, cam, st, fc, w, h)
+    dev = rt.DeviceScene(sc, 0)
+    try:
+        with dev.configured(traversal_ref=1):
+            _, gs = dev.render(cam, st, fc, w, h)
+    finally:
+        dev.close()
+    _, cs = ob.render(sc.desc(), cam, st, fc, w, h, rng_mode=0, threads=8)
+    REPORT["mesh_without_bvh_traversal_ref"] = check_traversal_ref(gs, cs)
+    for k in range(2):
+        assert gs.traversal_ref[k].mesh_intersection_count == cs.traversal[k].mesh_intersection_count
