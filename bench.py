@@ -51,7 +51,11 @@ METRIC = "Mrays/s + samples/s/GPU at 1080p 256spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E, MI355X_MICROARCH.md chip table
 L2_PEAK_GBS = 16800.0          # rows gathered from the XCDs' L2, chip-wide (MI355X_MICROARCH.md, lower bound)
 STAGES = ["generate", "extend", "shade", "connect", "splat", "resolve"]
-KERNEL = {"generate": "k_generate", "extend": "k_extend", "shade": "k_shade", "connect": "k_connect",
+# "extend" is the trace launch of an iteration's extension rays; with the merged shadow launch (r06,
+# rt_scene_config::shadow_launch: a rank's share of a multi-GPU frame) it also traces the previous
+# iteration's shadow rays and "connect" (RT_KERNEL_CONNECT) has no launches; otherwise "connect" is the
+# separate shadow launch
+KERNEL = {"generate": "k_generate", "extend": "k_trace", "shade": "k_shade", "connect": "k_trace_shadow",
           "splat": "k_splat", "resolve": "k_resolve"}
 # Algorithmic HBM bytes per unit of work, with the unit each launch processes:
 #   generate: a new path's ray (32 B) + path state (48 B) written                  per sample
@@ -60,6 +64,18 @@ KERNEL = {"generate": "k_generate", "extend": "k_extend", "shade": "k_shade", "c
 #   connect:  the shadow record (48 B) + contribution (16 B) in                   per traced shadow ray
 #   splat:    path state 48 B in, the 16 B sample record out                      per sample
 BYTES_PER_UNIT = {"generate": 80, "extend": 68, "shade": 192, "connect": 64, "splat": 64}
+
+
+def stage_work(stage, samples, closest, traced, traced_sh, merged):
+    """(units, algorithmic bytes) of a stage's launches over some frames.  merged (no separate shadow
+    launches): the trace launch ("extend") does the traced closest-hit rays (68 B) and the traced shadow
+    rays (64 B)."""
+    if stage == "extend" and merged:
+        return traced + traced_sh, BYTES_PER_UNIT["extend"] * traced + BYTES_PER_UNIT["connect"] * traced_sh
+    if stage == "extend":
+        return traced, BYTES_PER_UNIT["extend"] * traced
+    units = {"generate": samples, "shade": closest, "connect": traced_sh, "splat": samples}[stage]
+    return units, BYTES_PER_UNIT[stage] * units
 # whole-pipeline figure of SURVEY.md §8(d): B_alg = 152 B per ray + 144 B per sample
 PIPE_BYTES_PER_RAY, PIPE_BYTES_PER_SAMPLE = 152, 144
 CONFIGS = {
@@ -157,12 +173,12 @@ def cpu_baseline(rt, cfg, spp_override, seconds_budget=15.0):
                       f"nproc {hc['nproc']}), {dt:.1f} s, {rays} rays; again at {t125} threads"}
 
 
-def pmc_figures(tj, kname, bytes_per_unit, units_per_frame, launches_per_frame):
+def pmc_figures(tj, kname, units_per_frame, alg, launches_per_frame):
     """The serialized (rocprofv3 --pmc) figures of kernel `kname` from one configuration's entry of
     profiles/traffic.json, normalized per frame over the same frame as the algorithmic bytes: the sum
     of the isolated durations and of the HBM bytes over ALL of the kernel's dispatches in one frame
-    (the early exits after a partition's end included) against bytes_per_unit x the units of one
-    frame.  `traffic` per launch divides the frame's counter bytes by the launches the units are
+    (the early exits after a partition's end included) against `alg`, the algorithmic bytes of one
+    frame's units.  `traffic` per launch divides the frame's counter bytes by the launches the units are
     averaged over (the event-timed ones), so it is comparable with `achieved`.  None when the entry
     is missing or was measured on a frame of another size (units per frame off by more than 10 %)."""
     ent = (tj or {}).get("kernels", {}).get(kname)
@@ -172,7 +188,6 @@ def pmc_figures(tj, kname, bytes_per_unit, units_per_frame, launches_per_frame):
         return None
     if abs(upf / units_per_frame - 1.0) > 0.1:
         return None
-    alg = bytes_per_unit * units_per_frame
     disp = ent["dispatches"] / frames
     iso_s = ent["isolated_mean_us"] * 1e-6 * disp
     hbm = ent["hbm_bytes_per_launch"] * disp
@@ -181,8 +196,8 @@ def pmc_figures(tj, kname, bytes_per_unit, units_per_frame, launches_per_frame):
                          "mean_dispatch_ms": round(ent["isolated_mean_us"] / 1e3, 4),
                          "alg_bytes_per_frame": round(alg), "achieved": round(gbs, 1),
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "source": tj.get("source"),
-                         "normalization": "per frame: bytes_per_unit x units of one frame / the sum of the "
-                                          "kernel's serialized dispatch durations in one frame"},
+                         "normalization": "per frame: the algorithmic bytes of one frame's units / the sum of "
+                                          "the kernel's serialized dispatch durations in one frame"},
             "traffic": round(hbm / max(launches_per_frame, 1e-9)),
             "traffic_per_frame": round(hbm), "traffic_ratio": round(hbm / alg, 3)}
 
@@ -389,7 +404,7 @@ def main():
     c4 = None
     if args.c4_steps > 0 and args.config != "c4" and args.shard_of <= 1:
         c4scene, c4dev, c4st, _, c4acc, c4step = setup("c4", CONFIGS["c4"]["w"], CONFIGS["c4"]["h"], asset_dir)
-        # C4's roofline is k_extend's (the kernel with the most GPU time there): HIP
+        # C4's roofline is the trace launch's (k_trace, the kernel with the most GPU time there): HIP
         # events around the extend launches only, in the warm-up and the timed frames
         ext = STAGES.index("extend")
         rt.lib().rt_set_profiling_stages(1 << ext)
@@ -399,7 +414,8 @@ def main():
             dist.barrier()
         c0 = time.perf_counter()
         cr = [0, 0, 0]
-        cx = [0.0, 0, 0, 0]             # extend: event ms, launches, traced rays, trace steps
+        cx = [0.0, 0, 0, 0, 0, 0]       # trace launch: event ms, launches, traced closest / shadow rays, trace steps,
+                                        # separate shadow launches
         for _ in range(args.c4_steps):
             cs = c4step()
             cr[0] += cs.closest_hit_rays
@@ -408,7 +424,9 @@ def main():
             cx[0] += cs.kernel_ms[ext]
             cx[1] += cs.kernel_launches[ext]
             cx[2] += cs.traced_rays[0]
-            cx[3] += cs.trace_steps[0]
+            cx[3] += cs.traced_rays[1]
+            cx[5] += cs.kernel_launches[STAGES.index("connect")]
+            cx[4] += cs.trace_steps[0] + (cs.trace_steps[1] if not cx[5] else 0)
         torch.cuda.synchronize(device)
         if distributed:
             dist.barrier()
@@ -428,28 +446,30 @@ def main():
               "samples_per_s": round(float(crt[2]) / cel, 1),
               "samples_per_s_per_gpu": round(float(crt[2]) / cel / world, 1),
               "closest_hit_rays": int(crt[0]), "shadow_rays": int(crt[1])}
-        # rank 0's k_extend: 68 B per traced ray over the launches' HIP-event time;
-        # the serialized figures and counter traffic from profiles/traffic.json's c4 entry (same frame
-        # size only); the step fetches (128 B per trace step, the frames' own counts) against the L2 rate
+        # rank 0's trace launch (k_trace): 68 B per traced closest-hit ray + 64 B per traced shadow ray (SURVEY.md
+        # section 8(d)) over the launches' HIP-event time; the serialized figures and counter traffic from
+        # profiles/traffic.json's c4 entry (same frame size only); the step fetches (128 B per trace step, the
+        # frames' own counts) against the L2 rate
         if cx[1] and cx[0] > 0:
             n = args.c4_steps
             mean_s = cx[0] / cx[1] / 1e3
-            upl = cx[2] / cx[1]
-            gbs = BYTES_PER_UNIT["extend"] * upl / mean_s / 1e9
-            tgbs = 128.0 * cx[3] / cx[1] / mean_s / 1e9
-            pmc4 = pmc_figures(traffic_cfg("c4"), "k_extend", BYTES_PER_UNIT["extend"], cx[2] / n, cx[1] / n)
-            c4["roofline"] = {"bound": "hbm", "kernel": "k_extend", "bytes_per_unit": BYTES_PER_UNIT["extend"],
-                              "units_per_launch": round(upl, 1), "mean_launch_ms": round(mean_s * 1e3, 4),
+            u4, b4 = stage_work("extend", 0, 0, cx[2], cx[3], merged=not cx[5])
+            gbs = b4 / cx[1] / mean_s / 1e9
+            tgbs = 128.0 * cx[4] / cx[1] / mean_s / 1e9
+            k4 = "k_trace_ext" if cx[5] else "k_trace"
+            pmc4 = pmc_figures(traffic_cfg("c4"), k4, u4 / n, b4 / n, cx[1] / n)
+            c4["roofline"] = {"bound": "hbm", "kernel": k4, "bytes_per_unit": round(b4 / max(u4, 1), 2),
+                              "units_per_launch": round(u4 / cx[1], 1), "mean_launch_ms": round(mean_s * 1e3, 4),
                               "achieved": round(gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(gbs / HBM_PEAK_GBS, 6),
                               "traffic": pmc4["traffic"] if pmc4 else None,
                               "traffic_ratio": pmc4["traffic_ratio"] if pmc4 else None,
                               "isolated": pmc4["isolated"] if pmc4 else None,
-                              "traversal": {"bytes_per_step": 128, "steps_per_ray": round(cx[3] / max(cx[2], 1), 3),
+                              "traversal": {"bytes_per_step": 128, "steps_per_ray": round(cx[4] / max(u4, 1), 3),
                                             "achieved": round(tgbs, 1), "peak": L2_PEAK_GBS,
                                             "frac": round(tgbs / L2_PEAK_GBS, 4)},
-                              "timing": "HIP events around rank 0's extend launches in the timed C4 frames "
-                                        "(four partitions share the GPU)"}
+                              "timing": "HIP events around rank 0's trace launches in the timed C4 frames "
+                                        "(four partitions share the GPU); units: traced closest-hit + shadow rays"}
 
     if rank == 0:
         rays = closest_all + shadow_all
@@ -460,14 +480,17 @@ def main():
         # time it shares with the other partitions' kernels: `concurrency` says how many
         # kernels ran at once on average, and `isolated` gives the serialized figures
         # (rocprofv3 --pmc runs, profiles/traffic.json) for the same kernel.
-        units = {"generate": samples, "extend": traced, "shade": closest, "connect": traced_sh, "splat": samples}
+        merged = not (kl[STAGES.index("connect")] or wl[STAGES.index("connect")])   # no separate shadow launches
+        if not merged:
+            KERNEL.update({"extend": "k_trace_ext", "connect": "k_trace_shadow"})
+        work = {k: stage_work(k, samples, closest, traced, traced_sh, merged) for k in BYTES_PER_UNIT}
         dom = max(BYTES_PER_UNIT, key=lambda k: kms[STAGES.index(k)])     # the only stage timed (warm-up > 0)
         di = STAGES.index(dom)
         mean_launch_s = (kms[di] / 1e3) / max(kl[di], 1)
-        units_per_launch = units[dom] / max(kl[di], 1)
-        alg_bytes = BYTES_PER_UNIT[dom] * units_per_launch
+        units_per_launch = work[dom][0] / max(kl[di], 1)
+        alg_bytes = work[dom][1] / max(kl[di], 1)
         achieved = alg_bytes / mean_launch_s / 1e9 if mean_launch_s > 0 else 0.0
-        pmc = pmc_figures(traffic_cfg(args.config), KERNEL[dom], BYTES_PER_UNIT[dom], units[dom] / args.steps,
+        pmc = pmc_figures(traffic_cfg(args.config), KERNEL[dom], work[dom][0] / args.steps, work[dom][1] / args.steps,
                           kl[di] / args.steps)
         traffic = pmc["traffic"] if pmc else None
         isolated = pmc["isolated"] if pmc else None
@@ -480,19 +503,26 @@ def main():
         traversal = None
         if args.warmup:
             traversal = {"peak": L2_PEAK_GBS, "unit": "GB/s", "bytes_per_step": 128,
-                         "source": "rt_stats::trace_steps of the timed frames (counted on the device; the extend / connect launches' own steps, the fused drain's left out)",
+                         "source": "rt_stats::trace_steps of the timed frames (counted on the device; the trace launches' "
+                                   "own steps, closest-hit and shadow, the fused drain's left out)",
                          "timing": "warm-up frames, HIP events on each partition's stream (shared GPU)"}
-            for kind, (stage, kname, rays) in enumerate((("extend", "k_extend", traced), ("connect", "k_connect", traced_sh))):
+            # the trace launch (merged: both kinds of ray), and the separate shadow launch when there is one
+            kinds = [("extend", "k_trace", traced + traced_sh if merged else traced,
+                      steps_k[0] + steps_k[1] if merged else steps_k[0])]
+            if not merged:
+                kinds[0] = ("extend", "k_trace_ext", traced, steps_k[0])
+                kinds.append(("connect", "k_trace_shadow", traced_sh, steps_k[1]))
+            for stage, kname, rays, ksteps in kinds:
                 k = STAGES.index(stage)
                 if not wl[k] or wms[k] <= 0 or not rays:
                     continue
                 launches = wl[k] / args.warmup                     # per frame
-                steps = steps_k[kind] / args.steps                  # per frame
+                steps = ksteps / args.steps                         # per frame
                 tb = 128.0 * steps / launches
                 mean_s = wms[k] / launches / 1e3
                 t_gbs = tb / mean_s / 1e9
                 traversal[kname] = {"rays_per_launch": round(rays / args.steps / launches),
-                                    "steps_per_ray": round(steps_k[kind] / rays, 3),
+                                    "steps_per_ray": round(ksteps / rays, 3),
                                     "bytes_per_launch": round(tb), "mean_launch_ms": round(mean_s * 1e3, 4),
                                     "achieved": round(t_gbs, 1), "frac": round(t_gbs / L2_PEAK_GBS, 4)}
         ref = wms if args.warmup else [x / args.steps for x in kms]        # all stages: warm-up frames
@@ -547,8 +577,9 @@ def main():
             "traced_rays": [int(traced_all), int(traced_sh_all)],
             # rank 0's units of work per frame per kernel (tools/pmc_summary.py --traffic keeps them with
             # the PMC figures, which bench.py uses only for frames of the same size)
-            "units_per_frame": {KERNEL[k]: round(units[k] / args.steps, 1) for k in ("generate", "extend", "shade",
-                                                                                      "connect")},
+            "units_per_frame": {KERNEL[k]: round(work[k][0] / args.steps, 1)
+                                for k in ("generate", "extend", "shade") + (() if merged else ("connect",))},
+            "shadow_launch": "merged into the trace launch" if merged else "separate",
             "config": {"workload": f"{args.config}: {cfg['preset']} {w}x{h} {st.samples_per_pixel}spp "
                                    f"depth {st.max_bounce_count}" + (" env-sampling" if args.env_sampling else ""),
                        "width": w, "height": h,
@@ -561,7 +592,7 @@ def main():
                                       "(DESIGN.md section 7)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "kernel": KERNEL[dom], "bytes_per_unit": BYTES_PER_UNIT[dom],
+                         "kernel": KERNEL[dom], "bytes_per_unit": round(alg_bytes / max(units_per_launch, 1e-9), 2),
                          "units_per_launch": round(units_per_launch, 1),
                          "mean_launch_ms": round(mean_launch_s * 1e3, 4),
                          "traffic_ratio": pmc["traffic_ratio"] if pmc else None,

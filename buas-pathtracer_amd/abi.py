@@ -26,6 +26,7 @@ RT_PRIMITIVE_NONE, RT_PRIMITIVE_PLANE, RT_PRIMITIVE_SPHERE, RT_PRIMITIVE_BOX, RT
 RT_SAMPLING_UNIFORM, RT_SAMPLING_OPTIMIZED_BLUE_NOISE, RT_SAMPLING_STRATIFIED = range(3)
 RT_SPLAT_STREAM, RT_SPLAT_EXACT, RT_SPLAT_ATOMIC = range(3)          # rt_splat_mode
 RT_SHARD_TILES, RT_SHARD_PASSES = range(2)                           # rt_shard_mode
+RT_SHADOW_LAUNCH_AUTO, RT_SHADOW_LAUNCH_SEPARATE, RT_SHADOW_LAUNCH_MERGED = range(3)   # rt_shadow_launch (ABI 8)
 RT_RNG_PER_SAMPLE, RT_RNG_TILE_STREAM = 0, 1
 RT_HIT_MISS = 0xFFFFFFFF
 RT_HIT_PLANE_BIT = 0x80000000
@@ -176,8 +177,8 @@ class SceneConfig(C.Structure):       # rt_scene_config (per-scene schedule and 
                 ("partitions", C.c_int32), ("path_pool", C.c_int64), ("fuse_paths", C.c_int64),
                 ("splat_chunk", C.c_int32), ("splat_ring", C.c_int32), ("sample_budget_gb", C.c_double),
                 ("resolve_tall_pixels", C.c_int64), ("debug_traversal", C.c_int32), ("traversal_ref", C.c_int32),
-                ("drain_every", C.c_int32),                 # ABI 8
-                ("reserved", C.c_int32 * 5)]
+                ("drain_every", C.c_int32), ("shadow_launch", C.c_int32),  # ABI 8
+                ("reserved", C.c_int32 * 4)]
 
 
 class BvhInfo(C.Structure):

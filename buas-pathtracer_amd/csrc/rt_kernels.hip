@@ -3,15 +3,17 @@
 // Reference hot path (RT/ = /root/reference/Raytracer/):
 //   render_tile            RT/raytracer.cpp:366-495   -> k_generate (ray setup; splat of finished paths)
 //   advanced_integrator    RT/integrators.cpp:581-821 -> k_shade (one bounce per launch)
-//   intersect_scene        RT/intersection.cpp:606    -> k_extend
-//   intersect_shadow_ray   RT/intersection.cpp:600    -> k_connect
+//   intersect_scene        RT/intersection.cpp:606    -> k_trace (the extension queue)
+//   intersect_shadow_ray   RT/intersection.cpp:600    -> k_trace (the previous iteration's shadow queue)
 //   samplers / RNG         RT/samplers.{h,cpp}        -> rt_dmath.h + sample_1d/2d below
 //   splat_filter           RT/raytracer.cpp:187-259   -> splat_sample records + k_resolve
 //
 // Wavefront loop: a pool of N in-flight paths lives in HBM as
 // structure-of-arrays with a state byte per slot.  One iteration = generate ->
-// extend -> shade -> connect -> bookkeep, each a separate kernel (generate first
-// splats the paths the previous iteration finished).
+// trace -> shade -> bookkeep, each a separate kernel: trace takes this iteration's
+// extension rays and the previous shade's shadow rays, generate first splats the
+// paths the shade two iterations back finished (their last NEE terms came in the
+// trace in between).
 // generate / shade walk the pool in slot order; the two tracers
 // consume compacted queues (extension rays, shadow rays) that those kernels
 // append to with wave-aggregated atomics (__ballot + popcount + one atomic per
@@ -25,6 +27,7 @@
 #include <vector>
 #include <chrono>
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <mutex>
 #include <cerrno>
@@ -1240,15 +1243,23 @@ struct Pool {
     uint32_t  shard_cap; // queue entries per shard (queues are NSHARD shards of shard_cap)
     uint32_t* claim_base;// [blocks]: exclusive scan of the blocks' free slots (k_bookkeep: block_free) = first
                          // claim of the block
-    PathOut nx;          // the other buffer: k_shade's survivors, k_connect's NEE terms for them
+    PathOut nx;          // the other buffer: k_shade's survivors (the next k_trace adds their NEE terms)
     // finished paths, per wave of 64 slots compacted from the wave's first entry (k_shade; the next
-    // k_generate splats them, k_connect adds a pending last NEE term): {L, vignette}, {ray_d.w key,
+    // k_trace adds a pending last NEE term, the k_generate after it splats them): {L, vignette}, {ray_d.w key,
     // tile-list pixel p}, ray_o.w pixel; fin_w[wave] of them.  free_w[wave]: the wave's slots past
     // its survivors (block_free sums a block's four).  The AA jitter is recomputed (sample_jitter).
     float4*   fin_L;
     uint2*    fin_k;
     uint32_t* fin_px;
     uint32_t* fin_w;
+    // The finished arrays are double-buffered with the path buffers (r06): k_shade writes the set of its
+    // iteration's parity, and the k_trace of the next iteration adds the last NEE terms of its paths
+    // (their shadow rays ride in that launch), so they are splatted by the k_generate two iterations on,
+    // which sees that set as its own again.  fin2_*: the other set (the previous k_shade's).
+    float4*   fin2_L;
+    uint2*    fin2_k;
+    uint32_t* fin2_px;
+    uint32_t* fin2_w;
     uint32_t* free_w;
     // This partition's sample records (the deterministic splats): pass s, tile-list pixel p at
     // ((s - rec_pass0) % rec_ring)*P + p.  A ring of rec_ring passes in the streaming splat
@@ -1279,20 +1290,23 @@ constexpr int NXCD = 8;                        // MI355X: workgroups are dealt r
 constexpr int LINE_WORDS = 32;
 struct Counters {
     uint32_t ext_count[2][NSHARD][LINE_WORDS];   // extension queue length per shard (ping-pong)
-    uint32_t shadow_count[NSHARD][LINE_WORDS];   // shadow queue length per shard
+    uint32_t shadow_count[2][NSHARD][LINE_WORDS];   // shadow queue length per shard, by the path buffer parity of the
+                                                    // k_shade that made it (the next iteration's k_trace traces it)
     uint32_t fetch[2][NSHARD][LINE_WORDS];       // persistent trace kernels: items handed out (extend, connect)
     uint32_t cast[2][NSHARD][LINE_WORDS];        // rays cast this iteration: [1] shadow (k_shade); [0] unused since r03 (k_bookkeep counts the camera rays from the claims)
     uint32_t alive[NSHARD][LINE_WORDS];          // paths k_shade continued (each casts a closest ray next iteration)
-    uint32_t unsplat[NSHARD][LINE_WORDS];        // paths finished this iteration, splatted by the next k_generate
+    uint32_t unsplat[NSHARD][LINE_WORDS];        // paths finished this iteration, splatted by the k_generate after next
+    uint32_t unsplat_prev;                       // the previous iteration's (k_bookkeep): splatted by the next k_generate
     uint32_t gen_free;              // free slots counted by the last k_bookkeep = claims of the next k_generate
     uint32_t pending;               // paths queued for the next iteration (host termination test)
-    uint32_t pending_splat;         // finished paths the next k_generate splats (host termination test)
+    uint32_t pending_splat;         // finished paths not yet splatted and shadow rays not yet traced (host termination test)
     uint32_t cancel;
     uint32_t done;                  // every sample claimed, traced and splatted (k_bookkeep); the launches
                                     // still queued behind it (drain mode) exit at once
     uint32_t fused;                 // nothing left to claim and few paths alive (k_bookkeep): the next
                                     // iteration launched with the drain kernels runs every remaining
                                     // path to its end in k_drain; its extend / shade / connect exit
+    uint32_t drained;               // k_drain_list ran (it splatted the previous k_shade's finished paths)
     uint32_t drain_count[NSHARD][LINE_WORDS];   // k_drain_list: live slots per shard (in Pool::sh_slot)
     uint32_t drain_fetch[NSHARD][LINE_WORDS];   // k_drain: items handed out per shard
     // TraversalStats of the frame (rt_stats::traversal), per ray kind (0 closest, 1 shadow): TV_* counts,
@@ -1661,8 +1675,8 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_
             x = xy & 0xFFFFu; y = xy >> 16; s = pass;
         }
     }
-    // The paths the last k_shade finished in this wave's slots (its finished array, compacted):
-    // splat them.  Their NEE contributions from k_connect are in by now.
+    // The paths the k_shade two iterations back finished in this wave's slots (its finished array,
+    // compacted): splat them.  Their last NEE contributions came in the k_trace in between.
     if (lane < pool.fin_w[wbase]) {
         const float4 fl = ldnt(&pool.fin_L[slot]);
         const uint2 fk = ldnt(&pool.fin_k[slot]);
@@ -1744,16 +1758,15 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_
 }
 
 
-// k_trace<false> — intersect_scene for every queued path (RT/intersection.cpp:606-610)
-// k_trace<true>  — intersect_shadow_ray for every queued shadow ray (:600-604,
-//                  RT/integrators.cpp:756); unoccluded NEE contributions are
-//                  added to the path's total_color.
+// k_trace (below) — intersect_scene for every queued path (RT/intersection.cpp:606-610), then
+// intersect_shadow_ray for every queued shadow ray (:600-604, RT/integrators.cpp:756); unoccluded
+// NEE contributions are added to the path's total_color.
 // Persistent waves: each wave grabs CHUNK_EXT / CHUNK_SH queue items with one atomic and
 // refills lanes whose query has finished from that chunk (Aila & Laine 2009,
 // for 64-wide waves), so lanes do not idle behind the wave's longest ray.
 constexpr int TB = 256;                     // threads per persistent trace block
 constexpr uint32_t CHUNK = 256;             // queue items a wave takes per fetch (k_drain)
-// k_trace<false> / k_trace<true>: 128 (r05).  Only ~13 % of the closest and ~5 % of the shadow rays enter a
+// extension / shadow items: 128 (r05).  Only ~13 % of the closest and ~5 % of the shadow rays enter a
 // BVH, so a launch has ~1 chunk of 256 per wave and its end waits on the waves holding the last ones; 128
 // gives a rank's share of 8 +3.5 %, the full C3 / C4 frames within +-0.3 %; 96 or a chunk sized per launch
 // for 2-3 fetches per wave less (profiles/r05_chunk_ab.txt).
@@ -1772,22 +1785,15 @@ constexpr size_t TRACE_LDS = sizeof(uint2)*TRACE_STACK_LDS*TB + sizeof(float2)*T
 // LST: every queued ray carries a mesh list (the scene's top level is walked in the
 // prologue and has no more mesh instances than MLIST_MAX, DevScene::listed_only), so
 // the kernel is built without the top-level walk.
-template <bool OCC, bool LST, bool REF = false>
-__global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill,
-                                                              int fuse) {
-    if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
-    // trace waves are latency bound and issue little; shade waves sharing the SIMD are
-    // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
-    // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
-    __builtin_amdgcn_s_setprio(1);
-    extern __shared__ uint2 trace_lds[];   // TRACE_LDS bytes: the stack, then the barycentrics
-    StackT<TRACE_STACK_LDS> st;
-    st.lds = trace_lds; st.spill = spill; st.bary = reinterpret_cast<float2*>(trace_lds + TRACE_STACK_LDS*TB);
-    st.lane = threadIdx.x; st.block = TB;
-    st.gtid = blockIdx.x*TB + threadIdx.x; st.nthreads = gridDim.x*TB;
-    __shared__ uint32_t qlen[NSHARD];
-    if (threadIdx.x < NSHARD) qlen[threadIdx.x] = OCC ? cnt->shadow_count[threadIdx.x][0] : cnt->ext_count[cur][threadIdx.x][0];
-    __syncthreads();
+// One queue of a trace launch: persistent waves take CHUNK items per atomic from the queue's NSHARD
+// shards (their own first, then the others) and refill lanes whose query has finished.  OCC = false:
+// the extension queue (intersect_scene, the hit record into the path's slot); OCC = true: the shadow
+// queue of the previous iteration's k_shade (intersect_shadow_ray; an unoccluded ray adds its NEE
+// term to its path's total_color: a survivor's, now in this iteration's path buffer, or a finished
+// path's entry of the other finished array, fin2).
+template <bool OCC, bool LST, bool REF>
+RT_D void trace_queue(const DevScene& sc, const Pool& pool, Counters* cnt, int cur, const StackT<TRACE_STACK_LDS>& st,
+                      const uint32_t* qlen) {
     constexpr uint32_t chunk = OCC ? CHUNK_SH : CHUNK_EXT;
     // a wave drains its own shard first, then the others (a plain read of a head
     // skips exhausted shards without an atomic)
@@ -1804,7 +1810,7 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
             if (!tr.occluded) {
                 const uint32_t slot = pool.sh_dst[item];
                 const float4 c = ldnt(&pool.sh_c[item]);
-                float4* const dst = (slot & SH_FIN) ? &pool.fin_L[slot & ~SH_FIN] : &pool.nx.L[slot];
+                float4* const dst = (slot & SH_FIN) ? &pool.fin2_L[slot & ~SH_FIN] : &pool.L[slot];
                 float4 L = ldnt(dst);
                 L.x = L.x + c.x; L.y = L.y + c.y; L.z = L.z + c.z;   // total_color += ... (:768)
                 stnt(dst, L);
@@ -1866,6 +1872,45 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     tally.flush(tr.acc);
     if (REF) tally.flush_ref(tr.rc);
     tally.commit(cnt->trav[blockIdx.x % NSHARD], OCC ? 1 : 0);
+}
+
+// k_trace — one persistent launch per iteration for both queues (r06): intersect_scene for this
+// iteration's extension queue (RT/intersection.cpp:606-610), then intersect_shadow_ray for the
+// shadow queue the previous k_shade left (:600-604, RT/integrators.cpp:756).  Each wave finishes its
+// extension items, then takes shadow items, so the shadow rays fill the extension queue's tail
+// instead of a launch (and a tail) of their own; the finished paths they add to are splatted one
+// iteration later for it (Pool::fin2).  The fused drain's iteration traces the shadow queue only.
+// PH: bit 0 the extension queue, bit 1 the shadow queue -- 3 merged (rt_scene_config::shadow_launch), 1 and 2
+// the separate launches (2 with a pool view whose L / fin2 are the survivors' and finished paths' of the
+// same iteration and cur flipped, run_frame).  Each is its own instantiation: the separate ones keep the
+// registers of one kind of query, and profiles tell the launches apart.
+template <bool LST, bool REF, int PH>
+__global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill,
+                                                              int fuse, uint32_t sh_pct) {
+    if (cnt->done) return;                          // uniform
+    // trace waves are latency bound and issue little; shade waves sharing the SIMD are
+    // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
+    // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
+    __builtin_amdgcn_s_setprio(1);
+    extern __shared__ uint2 trace_lds[];   // TRACE_LDS bytes: the stack, then the barycentrics
+    StackT<TRACE_STACK_LDS> st;
+    st.lds = trace_lds; st.spill = spill; st.bary = reinterpret_cast<float2*>(trace_lds + TRACE_STACK_LDS*TB);
+    st.lane = threadIdx.x; st.block = TB;
+    st.gtid = blockIdx.x*TB + threadIdx.x; st.nthreads = gridDim.x*TB;
+    // k_drain runs this iteration's extension rays once the drain is fused (uniform)
+    const bool ext = (PH & 1) && !(fuse && cnt->fused);
+    __shared__ uint32_t qlen[2][NSHARD];
+    if (threadIdx.x < NSHARD) {
+        qlen[0][threadIdx.x] = ext ? cnt->ext_count[cur][threadIdx.x][0] : 0u;
+        qlen[1][threadIdx.x] = cnt->shadow_count[cur ^ 1][threadIdx.x][0];
+    }
+    __syncthreads();
+    // the shadow queue after the extension items: sh_pct % of the blocks, spread evenly over the grid (and
+    // the XCDs); all of them when there is no extension phase (the fused drain's iteration, whose k_drain
+    // waits for it, and the separate shadow launch).  (Shadow items first: share of 8 -2 %, C3 / C4 +-0.5 %.)
+    const bool sh = (PH & 2) && (!ext || (blockIdx.x*sh_pct) % 100u < sh_pct);
+    if ((PH & 1) && ext) trace_queue<false, LST, REF>(sc, pool, cnt, cur, st, qlen[0]);
+    if ((PH & 2) && sh) trace_queue<true, LST, REF>(sc, pool, cnt, cur, st, qlen[1]);
 }
 
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
@@ -2071,7 +2116,6 @@ template <bool IN_LDS, bool ENV>
 __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                  Counters* cnt, int cur, int sparse, int fuse) {
     if (fuse && cnt->fused) return;                 // k_drain runs this iteration's paths (uniform)
-    if (cnt->done) return;                          // the partition is complete (see k_drain_list)
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     // The slot's state and path record are loaded before the scene copy, whatever the
     // state: the three round trips (state, record, LDS blob) overlap instead of running
@@ -2089,6 +2133,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         h4 = ldnt(&pool.hit[slot]); r4 = ldnt(&pool.rng[slot]); hw = ldnt(&pool.hit_w[slot]);
     };
     if (sparse) {
+        if (cnt->done) return;                                          // uniform: every block reads it
         if (slot < pool.n) {
             state0 = pool.state[slot];
             if (state0 != S_FREE) load_path();
@@ -2171,7 +2216,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         const uint32_t nflags = pack_flags(bounce, is_spec, (uint32_t)at);
         if (cast_shadow) {
             // intersect_shadow_ray (:756): planes and the top level here; only rays that meet
-            // a mesh are queued for k_trace<true>.  Nothing else adds to total_color after the
+            // a mesh are queued for the next iteration's k_trace.  Nothing else adds to total_color after the
             // NEE term in a bounce, so adding it here keeps the reference's order (:768).
             spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
             sh_calls[threadIdx.x] = (uint8_t)spro.calls;   // counted at the tail, not held in a register
@@ -2232,7 +2277,7 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
         uint32_t* ap = nullptr;
         uint32_t av = 0;
         if (lane == 0) { ap = &cnt->ext_count[nxt][shard][0]; av = (uint32_t)__popcll(emask); }
-        if (lane == 1) { ap = &cnt->shadow_count[shard][0]; av = (uint32_t)__popcll(smask); }
+        if (lane == 1) { ap = &cnt->shadow_count[cur][shard][0]; av = (uint32_t)__popcll(smask); }
         uint32_t got = 0;
         if (av) got = atomicAdd(ap, av);
         // the other counters, no-return: alive, shadow rays cast, finished; the mesh instances reached
@@ -2278,11 +2323,12 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
 // separate kernels run (ray_prologue, Traversal, shade_bounce, splat_sample), so a path's
 // result is the same bits; the order in which paths finish does not enter any result.
 //
-// k_drain_list (the fused iteration, after k_generate splatted the last finished array): the
-// survivors of the last k_shade (S_TRACE) go to Pool::sh_slot, sharded like the queues; the
-// finished arrays are emptied (their entries are splatted already), and the pool is retired:
-// every wave's free count goes to 64, so a k_generate launched after the drain marks every slot
-// of whichever buffer it gets S_FREE.
+// k_drain_list (the fused iteration, after k_generate splatted the finished array of two iterations
+// back and k_trace added the last NEE terms of the last k_shade's): it splats the last k_shade's
+// finished paths (Pool::fin2, which the next k_generate would have splatted), the survivors of that
+// k_shade (S_TRACE) go to Pool::sh_slot, sharded like the queues; both finished arrays are emptied,
+// and the pool is retired: every wave's free count goes to 64, so a k_generate launched after the
+// drain marks every slot of whichever buffer it gets S_FREE.
 //
 // Why the retirement (r06; the r05 every-4th-iteration carry lost the radiance of 13,120 samples
 // of one claim batch on C4-small).  k_drain leaves the pool states as they were, and free_w keeps
@@ -2295,13 +2341,27 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
 // the re-runs splatted the poorer results over the finished records.  The default
 // schedule never ran into it only because every iteration after the first fused one carried the drain
 // kernels, whose fuse flag makes extend / shade / connect exit.  Now the drain leaves no live state
-// behind, and k_generate / k_shade exit once Counters::done is set, whatever the host's cadence.
-__global__ void __launch_bounds__(BLOCK) k_drain_list(Pool pool, Counters* cnt) {
+// behind (and k_generate exits once Counters::done is set), whatever the host's cadence.  (A done
+// check in k_shade itself costs it an 8-byte spill at 64 VGPRs: the retired pool makes it unneeded.)
+__global__ void __launch_bounds__(BLOCK) k_drain_list(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
+                                                      int splat_prev) {
     if (!cnt->fused || cnt->done) return;                              // uniform
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const uint8_t stv = slot < pool.n ? pool.state[slot] : S_FREE;
     const bool live = stv == S_TRACE || stv == S_NEW;
-    if (slot < pool.n && (slot & 63u) == 0) { pool.fin_w[slot >> 6] = 0; pool.free_w[slot >> 6] = 64; }
+    const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
+    if (splat_prev && slot < pool.n && __lane_id() < pool.fin2_w[wbase]) {   // as k_generate splats (fin2: its set)
+        const float4 fl = ldnt(&pool.fin2_L[slot]);
+        const uint2 fk = ldnt(&pool.fin2_k[slot]);
+        const uint32_t pixel = ldnt(&pool.fin2_px[slot]);
+        const uint32_t fs = fp.list_xy ? fp.list_s[fk.x] : fk.x;
+        const V2 j = sample_jitter(sc, st, fp, pixel & 0xFFFFu, pixel >> 16, fs);
+        splat_sample(fp, pool, ld3(fl), fl.w, make_float2(j.x, j.y), fk.x, fk.y);
+    }
+    if (slot < pool.n && (slot & 63u) == 0) {
+        pool.fin_w[slot >> 6] = 0; pool.fin2_w[slot >> 6] = 0; pool.free_w[slot >> 6] = 64;
+    }
+    if (slot == 0) cnt->drained = 1;
     const uint32_t shard = blockIdx.x % NSHARD;
     __shared__ uint32_t tally[(BLOCK / 64 + 2)*1];
     const bool tp[1] = {live};
@@ -2431,7 +2491,7 @@ __global__ void __launch_bounds__(DTB) k_drain(DevScene sc, rt_settings st, Fram
                                      cast_shadow, sh_o, sh_d, sh_c, sh_t, sh_light);
         }
         // intersect_shadow_ray (:756): the prologue, then the BVH walk; the NEE term is added last
-        // in the bounce, as k_connect adds it (:768)
+        // in the bounce, as k_trace adds it (:768)
         {
             Prologue spro = {};
             if (cast_shadow) spro = ray_prologue(sc, sh_o, sh_d, sh_t, true, sh_light);
@@ -2768,7 +2828,9 @@ enum { BK_ITER = 0, BK_FIRST = 1, BK_FINAL = 2 };
 // (0: never; see k_drain)
 // cast0: max_bounce_count > 0, so every sample claimed this iteration casts a camera ray (k_bookkeep counts
 // them from the claims; k_generate keeps no counter for them)
-struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0; };
+// merged: the shadow rays ride in the next iteration's trace launch (TraceMode): the previous k_shade's
+// finished paths are splatted one iteration later, and the shadow queue of this iteration is still pending
+struct ResPlan { uint32_t mode, P, pass1, ring, chunk, life, fuse, cast0, merged; };
 // Two workgroup sizes, picked per frame by the partition's pool (BK_LARGE_POOL): a pool of 4M paths or
 // more (a whole 1080p frame: 8.4M) takes the 512-thread build (92 VGPRs: 8 waves that find room beside
 // the other partitions' kernels sooner), a smaller one (a rank's share of a multi-GPU frame: 3.3M) the
@@ -2817,19 +2879,23 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
         // partitions' kernels, 10 % of a partition's iteration.)
         const bool it_phase = phase == BK_ITER;
         const uint32_t done_flag = it_phase ? cnt->done : 0u;
-        uint32_t al = 0, c1 = 0, us = 0, eq = 0, sq = 0;
+        // sq: the shadow queue this iteration's k_trace traced (the previous k_shade's); sp: the one this
+        // iteration's k_shade left for the next k_trace
+        uint32_t al = 0, c1 = 0, us = 0, eq = 0, sq = 0, sp = 0;
         if (it_phase && t < NSHARD) {
             al = cnt->alive[t][0];
             c1 = cnt->cast[1][t][0];
             us = cnt->unsplat[t][0];
             eq = cnt->ext_count[cur][t][0];
-            sq = cnt->shadow_count[t][0];
+            sq = cnt->shadow_count[plan.merged ? cur ^ 1 : cur][t][0];
+            sp = plan.merged ? cnt->shadow_count[cur][t][0] : 0u;
         }
         unsigned long long next = 0, total = 0, lim = 0, start = 0;
-        uint32_t gfree = 0, it = 0, rcur = 0;
+        uint32_t gfree = 0, it = 0, rcur = 0, us_prev = 0, drained = 0;
         if (t == 0 && it_phase) {
             next = cnt->next_sample; total = cnt->total_samples; lim = cnt->claim_limit;
             start = cnt->start_sample; gfree = cnt->gen_free; it = cnt->iter; rcur = cnt->res_cursor;
+            us_prev = cnt->unsplat_prev; drained = cnt->drained;
         }
         // the claim cursor `life` iterations ago (loaded before any store to the counters)
         const unsigned long long done_cursor =
@@ -2840,15 +2906,16 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
             cnt->cast[1][t][0] = 0;
             cnt->alive[t][0] = 0;
             cnt->ext_count[cur][t][0] = 0;
-            cnt->shadow_count[t][0] = 0;
+            cnt->shadow_count[plan.merged ? cur ^ 1 : cur][t][0] = 0;
             cnt->fetch[0][t][0] = 0;
             cnt->fetch[1][t][0] = 0;
         }
-        uint32_t ext = al, sh = c1, pend = al, ps = us, tq = eq, ts = sq;
+        uint32_t ext = al, sh = c1, pend = al, ps = us, tq = eq, ts = sq, spn = sp;
 #pragma unroll
         for (int off = 1; off < NSHARD; off <<= 1) {
             ext += __shfl_xor(ext, off); sh += __shfl_xor(sh, off); pend += __shfl_xor(pend, off);
             ps += __shfl_xor(ps, off); tq += __shfl_xor(tq, off); ts += __shfl_xor(ts, off);
+            spn += __shfl_xor(spn, off);
         }
         if (t == 0) {
             skip = sk;
@@ -2874,9 +2941,13 @@ __global__ void __launch_bounds__(BK_THREADS) k_bookkeep(Counters* cnt, Pool poo
                 cnt->traced_rays[0] += tq;
                 cnt->traced_rays[1] += ts;
                 cnt->pending = pend;
-                cnt->pending_splat = ps;
+                // still to splat: this iteration's finished paths and the previous one's (the fused drain's
+                // k_drain_list splatted those already), and the shadow rays the next k_trace traces for them
+                const uint32_t prev = (drained || !plan.merged) ? 0u : us_prev;
+                cnt->pending_splat = ps + prev + spn;
+                cnt->unsplat_prev = ps;
                 // nothing left to claim, trace or splat: every record is in the ring
-                const bool complete = next >= total && pend == 0 && ps == 0;
+                const bool complete = next >= total && pend == 0 && ps == 0 && prev == 0 && spn == 0;
                 if (complete) cnt->done = 1;
                 else if (plan.fuse && next >= total && pend <= plan.fuse) cnt->fused = 1;
                 cnt->iter = it + 1;
@@ -3078,9 +3149,10 @@ struct rt_scene {
     int32_t* d_tile_base = nullptr;
     size_t tile_base_cap = 0;
     uint32_t trace_grid = 0;        // persistent k_trace blocks (extend)
-    uint32_t connect_grid = 0;      // persistent k_trace<true> blocks (<= trace_grid: the spill area)
     uint32_t drain_grid = 0;        // persistent k_drain blocks (<= trace_grid: the spill area)
     uint32_t drain_lanes_full = 0;  // k_drain lanes of a grid that fills the GPU (the fused-drain threshold's unit)
+    uint32_t connect_grid = 0;      // the separate shadow launch's blocks (<= trace_grid: the spill area)
+    uint32_t shadow_pct = 100;      // the k_trace blocks that also take the shadow queue, in % (RT_SHADOW_PCT)
     float4* d_samp = nullptr;       // per-sample records for the deterministic splat
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
@@ -3305,6 +3377,10 @@ int ensure_pool(Partition& pt, uint32_t n) {
     e |= alloc((void**)&p.fin_L, 16*N);
     e |= alloc((void**)&p.fin_k, 8*N);
     e |= alloc((void**)&p.fin_px, 4*N);
+    e |= alloc((void**)&p.fin2_w, 4*(N / 64));
+    e |= alloc((void**)&p.fin2_L, 16*N);
+    e |= alloc((void**)&p.fin2_k, 8*N);
+    e |= alloc((void**)&p.fin2_px, 4*N);
     e |= alloc((void**)&p.nx.ray_o, 16*N);
     e |= alloc((void**)&p.nx.ray_d, 16*N);
     e |= alloc((void**)&p.nx.thr, 16*N);
@@ -3344,6 +3420,7 @@ Pool pool_view(const Pool& p, int par) {
     std::swap(v.L, v.nx.L); std::swap(v.prev_n, v.nx.prev_n);
     std::swap(v.rng, v.nx.rng); std::swap(v.hit, v.nx.hit); std::swap(v.hit_w, v.nx.hit_w);
     std::swap(v.mstack, v.nx.mstack); std::swap(v.state, v.nx.state);
+    std::swap(v.fin_L, v.fin2_L); std::swap(v.fin_k, v.fin2_k); std::swap(v.fin_px, v.fin2_px); std::swap(v.fin_w, v.fin2_w);
     return v;
 }
 
@@ -3426,7 +3503,7 @@ void launch_resolve_tiles(const SplatCfg& sp, const FrameParams& fp, const Pool&
 // passes into its own buffer while the frame renders (k_resolve_tiles after the
 // bookkeep of every chunk's last iteration), and the buffers are added at the end.
 int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long long total, hipStream_t stream,
-              const SplatCfg& sp, rt_stats* stats) {
+              const SplatCfg& sp, rt_stats* stats, bool shard) {
     auto t0 = std::chrono::steady_clock::now();
     const bool listed = fp.list_xy != nullptr;
     const FrameShape shape = frame_shape(s, total, listed ? 0u : sp.passes);
@@ -3505,6 +3582,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         HIP_OK(hipMemcpyAsync(pt.cnt, pt.cnt_host + NIF, sizeof(Counters), hipMemcpyHostToDevice, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.state, S_FREE, N, r.stream));
         HIP_OK(hipMemsetAsync(pt.pool.fin_w, 0, 4ull*N / 64, r.stream));
+        HIP_OK(hipMemsetAsync(pt.pool.fin2_w, 0, 4ull*N / 64, r.stream));
         HIP_OK(hipMemsetD32Async((hipDeviceptr_t)pt.pool.free_w, 64, N / 64, r.stream));
         launch_bookkeep(pt.cnt, pt.pool, r.grid, 0, BK_FIRST, ResPlan{}, r.stream);
         if (prof && !pt.events) {
@@ -3513,9 +3591,22 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             pt.events = true;
         }
     }
+    // How the shadow rays are traced (rt_scene_config::shadow_launch).  Merged: in the next iteration's trace
+    // launch, after its extension rays (one launch and one tail less per iteration; the finished paths are
+    // splatted an iteration later).  Separate: a trace launch of their own after k_shade (r05's schedule).
+    // Auto: merged for a rank's share of a multi-GPU frame and for small pools (under BK_LARGE_POOL), where
+    // an iteration is short and its launches' tails weigh most; separate for a whole frame on one GPU.  A/B
+    // (profiles/r06_shadow_launch_ab.txt), merged against separate: rank 0's C3 share of 8 32.8-33.0 ms against
+    // 34.1, of 4 61.7-61.9 against 62.7, of 2 116.4-117.0 against 117.9-119.1; the whole C3 frame within the
+    // box's noise; the whole C4 frame 174.8-175.5 against 171.6-171.7.
+    const bool merged = s->cfg.shadow_launch == RT_SHADOW_LAUNCH_MERGED ||
+                        (s->cfg.shadow_launch == RT_SHADOW_LAUNCH_AUTO && (shard || pool_n < BK_LARGE_POOL));
     auto plan_of = [&](int k, uint32_t mode) {
         const Run& r = run[k];
-        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, life, fuse_paths, st->max_bounce_count > 0 ? 1u : 0u};
+        // merged: a path's record is written two iterations after its last bounce (its shadow ray rides in the
+        // next k_trace, the k_generate after that splats it): life + 1
+        return ResPlan{mode, fp.pixels, r.pass1, r.ring, sp.chunk, merged ? life + 1 : life, fuse_paths,
+                       st->max_bounce_count > 0 ? 1u : 0u, merged ? 1u : 0u};
     };
     // Stage timing without extra host syncs: each iteration records begin/end
     // events into one of EV_SLOTS ring slots; a chunk's slots are read back when
@@ -3529,7 +3620,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         for (int i = 0; i < r.chunk_n[b]; ++i) {
             const int slot = (int)((r.chunk_first[b] + i) % EV_SLOTS);
             for (int kern = 0; kern < RT_KERNEL_COUNT; ++kern) {
-                if (!((prof >> kern) & 1u) || kern == RT_KERNEL_SPLAT) continue;
+                // (the splat runs inside k_generate; merged, the shadow rays inside k_trace: no events of their own)
+                if (!((prof >> kern) & 1u) || kern == RT_KERNEL_SPLAT || (merged && kern == RT_KERNEL_CONNECT)) continue;
                 if (kern == RT_KERNEL_RESOLVE && !r.res_ev[slot]) continue;
                 float ms = 0.0f;
                 if (hipEventElapsedTime(&ms, ev(k, slot, kern, 0), ev(k, slot, kern, 1)) == hipSuccess) {
@@ -3554,6 +3646,12 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         auto b = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 0), q); };
         auto e = [&](int kern) { if ((prof >> kern) & 1u) (void)hipEventRecord(ev(k, slot, kern, 1), q); };
         const Pool pv = pool_view(pt.pool, r.cur);        // the path buffers swap every iteration
+        // separate shadow launch: k_generate splats the previous k_shade's finished set (the view's fin2)
+        Pool pg = pv;
+        if (!merged) {
+            std::swap(pg.fin_L, pg.fin2_L); std::swap(pg.fin_k, pg.fin2_k);
+            std::swap(pg.fin_px, pg.fin2_px); std::swap(pg.fin_w, pg.fin2_w);
+        }
         const int sparse = r.drain ? 1 : 0;
         // near the drain every iteration carries the fused-drain kernels; they run only in the
         // iteration after k_bookkeep set Counters::fused, whose extend / shade / connect then exit
@@ -3561,10 +3659,21 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         const uint32_t every = s->cfg.drain_every > 0 ? (uint32_t)s->cfg.drain_every : 1u;
         const int fuse = (r.near && fuse_paths && r.iters % every == every - 1) ? 1 : 0;
         b(RT_KERNEL_GENERATE);
-        k_generate<<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, r.cur);
-        e(RT_KERNEL_GENERATE);
-        if (fuse) {
-            k_drain_list<<<r.grid, BLOCK, 0, q>>>(pv, pt.cnt);
+        k_generate<<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pg, pt.cnt, r.cur);
+        e(RT_KERNEL_GENERATE); b(RT_KERNEL_EXTEND);
+        // the trace launch: this iteration's extension rays (merged: then the previous k_shade's shadow rays)
+        auto trace = [&](auto ph, const Pool& tp, int tcur, uint32_t grid) {
+            constexpr int PH = decltype(ph)::value;
+            const uint32_t shp = s->shadow_pct;
+            if (ds.listed_only) k_trace<true, false, PH><<<grid, TB, TRACE_LDS, q>>>(ds, tp, pt.cnt, tcur, pt.spill, fuse, shp);
+            else if (ref) k_trace<false, true, PH><<<grid, TB, TRACE_LDS, q>>>(ds, tp, pt.cnt, tcur, pt.spill, fuse, shp);
+            else k_trace<false, false, PH><<<grid, TB, TRACE_LDS, q>>>(ds, tp, pt.cnt, tcur, pt.spill, fuse, shp);
+        };
+        if (merged) trace(std::integral_constant<int, 3>{}, pv, r.cur, s->trace_grid);
+        else trace(std::integral_constant<int, 1>{}, pv, r.cur, s->trace_grid);
+        e(RT_KERNEL_EXTEND);
+        if (fuse) {                      // the fused drain, after the shadow rays of the last k_shade are in
+            k_drain_list<<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, merged ? 1 : 0);
             if (ds.listed_only) {
                 if (env) k_drain<true, true><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
                 else k_drain<true, false><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
@@ -3576,11 +3685,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
                 else k_drain<false, false><<<s->drain_grid, DTB, 0, q>>>(ds, *st, fp, pv, pt.cnt, pt.spill);
             }
         }
-        b(RT_KERNEL_EXTEND);
-        if (ds.listed_only) k_trace<false, true><<<s->trace_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else if (ref) k_trace<false, false, true><<<s->trace_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else k_trace<false, false><<<s->trace_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        e(RT_KERNEL_EXTEND); b(RT_KERNEL_SHADE);
+        b(RT_KERNEL_SHADE);
         if (env) {
             if (ds.blob_q) k_shade<true, true><<<r.grid, BLOCK, 16*ds.blob_q, q>>>(ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
             else k_shade<false, true><<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
@@ -3589,11 +3694,17 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         } else {
             k_shade<false, false><<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, r.cur, sparse, fuse);
         }
-        e(RT_KERNEL_SHADE); b(RT_KERNEL_CONNECT);
-        if (ds.listed_only) k_trace<true, true><<<s->connect_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else if (ref) k_trace<true, false, true><<<s->connect_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        else k_trace<true, false><<<s->connect_grid, TB, TRACE_LDS, q>>>(ds, pv, pt.cnt, r.cur, pt.spill, fuse);
-        e(RT_KERNEL_CONNECT);
+        e(RT_KERNEL_SHADE);
+        if (!merged) {
+            // separate: this k_shade's shadow rays now; their NEE terms go to the survivors in the other
+            // buffer and to this iteration's finished set, and the queue is the one of this parity
+            Pool pc = pv;
+            pc.L = pv.nx.L;
+            pc.fin2_L = pv.fin_L;
+            b(RT_KERNEL_CONNECT);
+            trace(std::integral_constant<int, 2>{}, pc, r.cur ^ 1, s->connect_grid);
+            e(RT_KERNEL_CONNECT);
+        }
         // in the drain every iteration plans a resolve: the one after the bookkeep that finds the
         // partition complete resolves its last passes at once, without waiting for the host
         const bool res = stream_splat && (plan || r.drain);
@@ -3882,6 +3993,7 @@ int check_config(const rt_scene_config* c) {
     else if (c->resolve_tall_pixels < 0) bad = "resolve_tall_pixels";
     else if (c->traversal_ref != 0 && c->traversal_ref != 1) bad = "traversal_ref";
     else if (c->drain_every < 0 || c->drain_every > 1024) bad = "drain_every (0..1024)";
+    else if (c->shadow_launch < RT_SHADOW_LAUNCH_AUTO || c->shadow_launch > RT_SHADOW_LAUNCH_MERGED) bad = "shadow_launch";
     if (bad) { set_error(std::string("rt_scene_config: bad ") + bad); return RT_ERROR_INVALID; }
     return RT_OK;
 }
@@ -3928,6 +4040,7 @@ bool config_from_env(rt_scene_config& c) {
     if (num("RT_DEBUG_TRAVERSAL", 0, 1, v)) c.debug_traversal = (int32_t)v;
     if (num("RT_TRAVERSAL_REF", 0, 1, v)) c.traversal_ref = (int32_t)v;
     if (num("RT_DRAIN_EVERY", 0, 1024, v)) c.drain_every = (int32_t)v;
+    if (num("RT_SHADOW_LAUNCH", RT_SHADOW_LAUNCH_AUTO, RT_SHADOW_LAUNCH_MERGED, v)) c.shadow_launch = (int32_t)v;
     return ok;
 }
 
@@ -4281,7 +4394,7 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) != hipSuccess) { set_error("hipGetDeviceProperties"); return fail(RT_ERROR_DEVICE); }
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false>, TB, TRACE_LDS) != hipSuccess || per_cu < 1) per_cu = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_trace<false, false, 3>, TB, TRACE_LDS) != hipSuccess || per_cu < 1) per_cu = 1;
         s->trace_grid = (uint32_t)(prop.multiProcessorCount*per_cu);
         // Persistent trace blocks: 75 % of one full-occupancy wave of blocks (RT_TRACE_GRID_PCT).
         // Four partitions run their trace launches side by side; a full grid per launch left
@@ -4289,16 +4402,19 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         // pairs: 75 % +1.5 %, 60 % +0.9 %, 50 % +1.5 % (2 pairs), 150 % -0.8 %.  The spill
         // area is sized from the result.
         bool env_ok = true;
-        long long grid_pct = 75, connect_pct = 25, drain_pct = 100;
+        long long grid_pct = 75, connect_pct = 25, drain_pct = 100, shadow_pct = 33;
         env_int("rt_scene_upload", "RT_TRACE_GRID_PCT", 1, 1000, grid_pct, env_ok);
         env_int("rt_scene_upload", "RT_CONNECT_GRID_PCT", 1, 1000, connect_pct, env_ok);
+        env_int("rt_scene_upload", "RT_SHADOW_PCT", 1, 100, shadow_pct, env_ok);
+        s->shadow_pct = (uint32_t)shadow_pct;
         env_int("rt_scene_upload", "RT_DRAIN_GRID_PCT", 1, 100, drain_pct, env_ok);
         if (!env_ok) return fail(RT_ERROR_INVALID);
         const uint32_t full = s->trace_grid;
         s->trace_grid = std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)grid_pct / 100ull));
-        // Shadow-ray launches carry a quarter of the extension rays (~0.8 per lane of a 75 % grid):
+        // The separate shadow launch carries a quarter of the extension rays (~0.8 per lane of a 75 % grid):
         // a 25 % grid does them as fast and leaves the registers to the other partitions' kernels
-        // (C3: +0.6 %, 2 pairs; 40 / 55 % between).
+        // (C3: +0.6 %, 2 pairs; 40 / 55 % between).  Merged into the trace launch, a third of its blocks
+        // take them (RT_SHADOW_PCT; all blocks: C4 -1 %, the share of 8 -0.3 %, profiles/r06_shadow_launch_ab.txt).
         s->connect_grid = std::min(s->trace_grid,
                                    std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)connect_pct / 100ull)));
         int drain_cu = 0;     // k_drain holds ~220 VGPRs: 2 waves per SIMD; its grid is what fits at once
@@ -4506,13 +4622,18 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         if (sp.mode == RT_SPLAT_STREAM) {
             // a resolve every ~32M samples, and at least four per partition (a small shard, e.g. one
             // rank's eighth of a frame, would otherwise resolve all its passes after its drain); the
-            // ring holds the passes not yet resolved: the chunk, the claims of the iterations a path
-            // can live (about 5 pool fills) and slack
+            // ring holds the passes not yet resolved: the chunk, the claims of the iterations between
+            // a sample's claim and its record (the life of a path, max_bounce_count iterations, plus
+            // one: its last NEE term rides in the next k_trace), at most a pool fill each, and slack.
+            // (r05 sized it at 5 pool fills: C4's shorter paths claim ~0.4 of the pool per iteration,
+            // so its claims waited on the ring: a ring of 60 passes gave C4 1080p +1.9 %,
+            // profiles/r06_ring_ab.txt)
             const uint32_t per_part = (spp + shape.nparts - 1) / shape.nparts;
             sp.chunk = (uint32_t)std::min<unsigned long long>(std::max<unsigned long long>((32ull << 20) / fp.pixels, 1ull),
                                                                std::max(1u, per_part / 4));
             if (s->cfg.splat_chunk > 0) sp.chunk = (uint32_t)s->cfg.splat_chunk;
-            const unsigned long long lag = (5ull*shape.pool_n + fp.pixels - 1) / fp.pixels;
+            const unsigned long long fills = std::max<uint32_t>(st->max_bounce_count, 1u) + 1ull;
+            const unsigned long long lag = (fills*shape.pool_n + fp.pixels - 1) / fp.pixels;
             sp.ring = (uint32_t)std::min<unsigned long long>(sp.chunk + lag + 2ull, per_part);
             if (s->cfg.splat_ring > 0) sp.ring = (uint32_t)s->cfg.splat_ring;
             sp.chunk = std::min(sp.chunk, sp.ring);                   // the planner needs chunk <= ring
@@ -4633,7 +4754,7 @@ int rt_render_device(rt_scene* s, const rt_camera* camera, const rt_settings* st
         }
     }
     if (debug_timing()) fprintf(stderr, "[rt timing] rt_render_device: layout + splat plan %.3f ms\n", host_ms() - t_entry);
-    err = run_frame(s, st, fp, total, stream, sp, stats);
+    err = run_frame(s, st, fp, total, stream, sp, stats, tiles->shard_count > 1);
     if (debug_timing()) fprintf(stderr, "[rt timing] rt_render_device: frame done %.3f ms after entry\n", host_ms() - t_entry);
     if (err || sp.mode != RT_SPLAT_EXACT) {
         if (!err) HIP_OK(hipStreamSynchronize(stream));      // the frame (and its last resolve, combine) is done
@@ -4733,7 +4854,7 @@ int rt_trace_samples(rt_scene* s, const rt_camera* camera, const rt_settings* st
     fp.list_xy = d_xy; fp.list_s = d_s; fp.list_out = d_out;
     set_divisors(fp);
     fill_camera(fp, camera);
-    err = run_frame(s, st, fp, count, nullptr, SplatCfg{}, stats);
+    err = run_frame(s, st, fp, count, nullptr, SplatCfg{}, stats, false);
     if (!err && hipMemcpy(out, d_out, 20*(size_t)count, hipMemcpyDeviceToHost) != hipSuccess) { set_error("copy out"); err = RT_ERROR_DEVICE; }
     (void)hipFree(d_xy); (void)hipFree(d_s); (void)hipFree(d_out);
     return err;

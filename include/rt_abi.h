@@ -460,11 +460,22 @@ int rt_cancel(rt_scene* scene);
  * Two scenes in one process may differ.  rt_scene_upload starts a scene from
  * rt_scene_default_config(), then applies the test-override environment variables once
  * (RT_SPLAT, RT_PARTITIONS, RT_FUSE_PATHS, RT_SPLAT_CHUNK, RT_SPLAT_RING,
- * RT_SAMPLE_BUDGET_GB, RT_RES_TALL_PIXELS, RT_DEBUG_TRAVERSAL, RT_DRAIN_EVERY); nothing reads the
+ * RT_SAMPLE_BUDGET_GB, RT_RES_TALL_PIXELS, RT_DEBUG_TRAVERSAL, RT_DRAIN_EVERY, RT_SHADOW_LAUNCH);
+ * nothing reads the
  * environment per frame.  A field at RT_CONFIG_INHERIT follows the process-wide setter
  * above at each frame (rt_set_splat_mode / rt_set_shard_mode / rt_set_env_sampling /
  * rt_set_path_pool), so callers of those setters see no change. */
 #define RT_CONFIG_INHERIT (-1)
+/* rt_scene_config::shadow_launch (ABI 8): the shadow rays of an iteration's k_shade are traced in a launch
+ * of their own right after it (SEPARATE), or in the next iteration's trace launch after its extension rays
+ * (MERGED: one launch and one tail less per iteration; a finished path is splatted an iteration later).
+ * AUTO: merged for a shard of a multi-rank frame (rt_tile_set::shard_count > 1) and for path pools under
+ * 4M paths (small frames), separate for a whole frame on one GPU. */
+typedef enum rt_shadow_launch {
+    RT_SHADOW_LAUNCH_AUTO = 0,
+    RT_SHADOW_LAUNCH_SEPARATE = 1,
+    RT_SHADOW_LAUNCH_MERGED = 2
+} rt_shadow_launch;
 typedef struct rt_scene_config {
     int32_t  splat_mode;            /* rt_splat_mode, or RT_CONFIG_INHERIT                          */
     int32_t  shard_mode;            /* rt_shard_mode, or RT_CONFIG_INHERIT                          */
@@ -483,7 +494,9 @@ typedef struct rt_scene_config {
     int32_t  drain_every;           /* (ABI 8) fused-drain kernels ride on every Nth iteration once the
                                        host expects the drain (N >= 1; 0 = auto: every iteration).  A
                                        schedule knob for the tests: frames are identical for every N */
-    int32_t  reserved[5];
+    int32_t  shadow_launch;         /* (ABI 8) rt_shadow_launch: where the NEE shadow rays are traced.
+                                       Frames are identical for every value */
+    int32_t  reserved[4];
 } rt_scene_config;
 int rt_scene_default_config(rt_scene_config* out);
 int rt_scene_get_config(const rt_scene* scene, rt_scene_config* out);

@@ -84,4 +84,4 @@ def test_scene_config_defaults(rt):
     assert (c.splat_mode, c.shard_mode, c.env_sampling) == (a.RT_CONFIG_INHERIT,) * 3
     assert (c.partitions, c.path_pool, c.fuse_paths, c.splat_chunk, c.splat_ring) == (0, 0, -1, 0, 0)
     assert c.sample_budget_gb < 0 and c.resolve_tall_pixels == 0 and c.debug_traversal == 0
-    assert c.traversal_ref == 0 and c.drain_every == 0
+    assert c.traversal_ref == 0 and c.drain_every == 0 and c.shadow_launch == a.RT_SHADOW_LAUNCH_AUTO

@@ -301,7 +301,7 @@ def test_scene_config_is_per_scene(rt, monkeypatch):
 @pytest.mark.parametrize("var,value", [("RT_SPLAT", "exact"), ("RT_SPLAT", "3"), ("RT_PARTITIONS", "9"),
                                        ("RT_FUSE_PATHS", "-1"), ("RT_SAMPLE_BUDGET_GB", "lots"),
                                        ("RT_TOP_PROLOGUE", "off"), ("RT_MLIST_MAX", "9"), ("RT_LDS_SCENE", "no"),
-                                       ("RT_TRACE_GRID_PCT", "0"), ("RT_CONNECT_GRID_PCT", "75%"),
+                                       ("RT_TRACE_GRID_PCT", "0"), ("RT_DRAIN_GRID_PCT", "75%"),
                                        ("RT_DRAIN_GRID_PCT", "200")])
 def test_bad_override_rejected(rt, monkeypatch, var, value):
     """A malformed test-override variable fails rt_scene_upload with RT_ERROR_INVALID naming it,

@@ -426,8 +426,9 @@ def test_fused_drain_matches_separate_kernels(which, w, h, spp, request):
     assert out["all"][4] < out["off"][4]          # the fused drain ended the frame in fewer iterations
 
 
+@pytest.mark.parametrize("mode", ["separate", "merged"])
 @pytest.mark.parametrize("which", ["c3small", "c4small"])
-def test_fused_drain_any_cadence(which, request):
+def test_fused_drain_any_cadence(which, mode, request):
     """Counters::fused is safe whatever iterations carry the drain kernels (rt_scene_config::
     drain_every, r06).  With the drain kernels on only every 2nd ... 7th iteration, k_bookkeep sets
     `fused` in iterations that run the separate extend / shade / connect launches, and iterations
@@ -440,9 +441,10 @@ def test_fused_drain_any_cadence(which, request):
     w, h = 192, 108
     rng = np.random.default_rng(13)
     xy, s = _sample_list(rng, w, h, 20000, st.samples_per_pixel)
+    launch = rt.abi.RT_SHADOW_LAUNCH_SEPARATE if mode == "separate" else rt.abi.RT_SHADOW_LAUNCH_MERGED
 
     def run(**cfg):
-        with dev.configured(splat_mode=rt.abi.RT_SPLAT_EXACT, **cfg):
+        with dev.configured(splat_mode=rt.abi.RT_SPLAT_EXACT, shadow_launch=launch, **cfg):
             fr, fs = dev.render(cam, st, fc, w, h)
             samp, ss = dev.trace_samples(cam, st, w, h, xy, s)
         rays = [(int(x.closest_hit_rays), int(x.shadow_rays), int(x.traced_rays[0]), int(x.traced_rays[1]))
@@ -461,7 +463,38 @@ def test_fused_drain_any_cadence(which, request):
             assert rays == ref[2], (every, fuse)
             assert np.array_equal(fr, ref[0]), (every, fuse, same)
             assert np.array_equal(samp, ref[1]), (every, fuse)
-    REPORT[f"fused_drain_cadence_{which}"] = report
+    REPORT[f"fused_drain_cadence_{which}_{mode}"] = report
+
+
+@pytest.mark.parametrize("which", ["c1", "c3small", "c4small"])
+def test_shadow_launch_modes_identical(which, request):
+    """rt_scene_config::shadow_launch (r06): the NEE shadow rays traced in a launch of their own after
+    k_shade (SEPARATE, the full frame's default) or in the next iteration's trace launch (MERGED, the
+    default of small pools) give the same bits: exact-splat frames (equal to the oracle's single-thread
+    frame on >= 99.9 % of pixels), streaming frames, per-sample radiance, ray counts, TraversalStats."""
+    rt, scene, cam, st, fc, dev = request.getfixturevalue(which)
+    w, h = (256, 256) if which == "c1" else (192, 108)
+    rng = np.random.default_rng(31)
+    xy, s = _sample_list(rng, w, h, 20000, st.samples_per_pixel)
+    out = {}
+    for name, launch in (("separate", rt.abi.RT_SHADOW_LAUNCH_SEPARATE), ("merged", rt.abi.RT_SHADOW_LAUNCH_MERGED)):
+        with dev.configured(shadow_launch=launch):
+            with dev.configured(splat_mode=rt.abi.RT_SPLAT_EXACT):
+                ex, es = dev.render(cam, st, fc, w, h)
+            sm, ss = dev.render(cam, st, fc, w, h)
+            samp, ts = dev.trace_samples(cam, st, w, h, xy, s)
+        stats = [(int(x.closest_hit_rays), int(x.shadow_rays), int(x.traced_rays[0]), int(x.traced_rays[1]),
+                  [x.traversal[k].as_dict() for k in range(2)]) for x in (es, ss, ts)]
+        out[name] = (ex, sm, samp, stats, int(ss.iterations))
+    cpu, _ = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1)
+    a, b = out["separate"], out["merged"]
+    REPORT[f"shadow_launch_{which}"] = {"frames_equal": bool(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])),
+                                        "samples_equal": bool(np.array_equal(a[2], b[2])), "stats_equal": a[3] == b[3],
+                                        "iterations": [a[4], b[4]],
+                                        "separate_pixels_vs_oracle": float(np.all(a[0] == cpu, axis=2).mean())}
+    assert a[3] == b[3]
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
+    assert np.all(a[0] == cpu, axis=2).mean() >= 0.999
 
 
 @pytest.mark.parametrize("depth", [0, 1, 2])

@@ -18,14 +18,21 @@ import glob
 import json
 import os
 
-KERNELS = ["k_generate", "k_trace<false", "k_shade", "k_trace<true", "k_splat", "k_resolve_tiles", "k_resolve",
-           "k_combine_partials", "k_bookkeep", "k_drain_list", "k_drain"]
-LABEL = {"k_trace<false": "k_extend (k_trace<false, .>)", "k_trace<true": "k_connect (k_trace<true, .>)"}
-KEYS = {"k_trace<false": "k_extend", "k_trace<true": "k_connect"}
+# r06: k_trace<LST, REF, PH>: PH 3 the merged trace launch (the extension rays, then the previous iteration's
+# shadow rays), 1 / 2 the separate extension / shadow launches (rt_scene_config::shadow_launch)
+KERNELS = ["k_generate", "k_trace", "k_trace_ext", "k_trace_shadow", "k_shade", "k_splat", "k_resolve_tiles",
+           "k_resolve", "k_combine_partials", "k_bookkeep", "k_drain_list", "k_drain"]
+LABEL = {"k_trace": "k_trace (merged: extension + shadow rays)", "k_trace_ext": "k_trace_ext (extension rays)",
+         "k_trace_shadow": "k_trace_shadow (shadow rays)"}
+KEYS = {}
 
 
 def short(name):
-    for k in KERNELS:
+    if "k_trace<" in name:                      # by the phases argument: void k_trace<true, false, 3>(...)
+        ph = name.split("k_trace<")[1].split(">")[0].split(",")[-1].strip()
+        return {"1": "k_trace_ext", "2": "k_trace_shadow"}.get(ph, "k_trace")
+    # longest names first: k_resolve_tiles before k_resolve, k_drain_list before k_drain
+    for k in sorted(KERNELS, key=len, reverse=True):
         if k in name:
             return k
     return None

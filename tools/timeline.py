@@ -39,8 +39,7 @@ def main():
     print(" ".join(f"{x / bucket:.1f}" for x in busy))
     per = {}
     for r in fr:
-        n = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        n = n.split("<")[0] + ("<" + n.split("<")[1].split(",")[0] + ">" if "k_trace" in n else "")
+        n = short(r)
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
         c, tot = per.get(n, (0, 0.0))
         per[n] = (c + 1, tot + d)
@@ -73,7 +72,9 @@ def main():
 
 def short(r):
     n = r["Kernel_Name"].split("(")[0].replace("void ", "")
-    return n.split("<")[0] + ("<" + n.split("<")[1].split(",")[0] + ">" if "k_trace" in n else "")
+    if "k_trace<" in n:           # k_trace<LST, REF, PH>: PH 3 merged, 1 extension, 2 shadow (rt_scene_config::shadow_launch)
+        return {"1": "k_trace_ext", "2": "k_trace_shadow"}.get(n.split("<")[1].rstrip(">").split(",")[-1].strip(), "k_trace")
+    return n.split("<")[0]
 
 if __name__ == "__main__":
     main()
