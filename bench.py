@@ -330,6 +330,7 @@ def main():
     if os.environ.get("RT_BENCH_NO_STAGE_EVENTS"):
         rt.lib().rt_set_profiling(0)
     closest = shadow = samples = traced = traced_sh = 0
+    separate = 0                     # timed frames with the separate shadow launch (rt_stats::shadow_launch)
     steps_k = [0, 0]                 # trace steps (rt_stats::trace_steps) of the timed frames, per kind
     trav = [dict.fromkeys(rt.abi.TRAVERSAL_FIELDS, 0) for _ in range(2)]
     kms = [0.0] * 6
@@ -346,6 +347,7 @@ def main():
         samples += s.samples
         traced += s.traced_rays[0]
         traced_sh += s.traced_rays[1]
+        separate += s.shadow_launch == rt.abi.RT_SHADOW_LAUNCH_SEPARATE
         for k in range(2):
             steps_k[k] += s.trace_steps[k]
             for f in rt.abi.TRAVERSAL_FIELDS:
@@ -415,7 +417,7 @@ def main():
         c0 = time.perf_counter()
         cr = [0, 0, 0]
         cx = [0.0, 0, 0, 0, 0, 0]       # trace launch: event ms, launches, traced closest / shadow rays, trace steps,
-                                        # separate shadow launches
+                                        # frames with the separate shadow launch
         for _ in range(args.c4_steps):
             cs = c4step()
             cr[0] += cs.closest_hit_rays
@@ -425,7 +427,7 @@ def main():
             cx[1] += cs.kernel_launches[ext]
             cx[2] += cs.traced_rays[0]
             cx[3] += cs.traced_rays[1]
-            cx[5] += cs.kernel_launches[STAGES.index("connect")]
+            cx[5] += cs.shadow_launch == rt.abi.RT_SHADOW_LAUNCH_SEPARATE
             cx[4] += cs.trace_steps[0] + (cs.trace_steps[1] if not cx[5] else 0)
         torch.cuda.synchronize(device)
         if distributed:
@@ -480,7 +482,7 @@ def main():
         # time it shares with the other partitions' kernels: `concurrency` says how many
         # kernels ran at once on average, and `isolated` gives the serialized figures
         # (rocprofv3 --pmc runs, profiles/traffic.json) for the same kernel.
-        merged = not (kl[STAGES.index("connect")] or wl[STAGES.index("connect")])   # no separate shadow launches
+        merged = not separate                       # the frames' shadow rays rode in the trace launch
         if not merged:
             KERNEL.update({"extend": "k_trace_ext", "connect": "k_trace_shadow"})
         work = {k: stage_work(k, samples, closest, traced, traced_sh, merged) for k in BYTES_PER_UNIT}

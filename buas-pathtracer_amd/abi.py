@@ -137,7 +137,7 @@ class Stats(C.Structure):
     _fields_ = [("closest_hit_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("samples", C.c_uint64),
                 ("iterations", C.c_uint64), ("seconds", C.c_double),
                 ("kernel_ms", C.c_double * RT_KERNEL_COUNT), ("kernel_launches", C.c_uint64 * RT_KERNEL_COUNT),
-                ("traced_rays", C.c_uint64 * 2), ("splat_mode", C.c_int32), ("reserved", C.c_int32),
+                ("traced_rays", C.c_uint64 * 2), ("splat_mode", C.c_int32), ("shadow_launch", C.c_int32),
                 ("traversal", TraversalStats * 2), ("trace_steps", C.c_uint64 * 2),
                 ("traversal_ref", TraversalStats * 2)]       # ABI 7: rt_scene_config::traversal_ref
 

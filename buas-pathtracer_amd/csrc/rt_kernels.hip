@@ -3864,6 +3864,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
         stats->shadow_rays = sum.shadow_rays;
         stats->samples = total;
         stats->iterations = iters;
+        stats->shadow_launch = merged ? RT_SHADOW_LAUNCH_MERGED : RT_SHADOW_LAUNCH_SEPARATE;
         stats->seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int k = 0; k < RT_KERNEL_COUNT; ++k) { stats->kernel_ms[k] = kms[k]; stats->kernel_launches[k] = klaunch[k]; }
         stats->traced_rays[0] = sum.traced_rays[0];

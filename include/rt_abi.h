@@ -252,7 +252,7 @@ typedef struct rt_stats {
        the planes / top-level root test where they were made (GPU only) */
     uint64_t traced_rays[2];
     int32_t  splat_mode;            /* rt_splat_mode the frame used (rt_render / rt_render_device) */
-    int32_t  reserved;
+    int32_t  shadow_launch;         /* (ABI 8) rt_shadow_launch the frame used: SEPARATE or MERGED */
     /* TraversalStats of the frame (above) per query kind: [0] closest-hit (intersect_scene),
        [1] shadow (intersect_shadow_ray); the reference's totals are the sums of the two */
     rt_traversal_stats traversal[2];

@@ -485,6 +485,7 @@ def test_shadow_launch_modes_identical(which, request):
             samp, ts = dev.trace_samples(cam, st, w, h, xy, s)
         stats = [(int(x.closest_hit_rays), int(x.shadow_rays), int(x.traced_rays[0]), int(x.traced_rays[1]),
                   [x.traversal[k].as_dict() for k in range(2)]) for x in (es, ss, ts)]
+        assert es.shadow_launch == ss.shadow_launch == ts.shadow_launch == launch   # rt_stats reports the mode used
         out[name] = (ex, sm, samp, stats, int(ss.iterations))
     cpu, _ = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=1)
     a, b = out["separate"], out["merged"]
