@@ -1636,9 +1636,6 @@ RT_D V2 sample_jitter(const DevScene& sc, const rt_settings& st, const FramePara
 // of 8 +1.4 %, C3 / C4 +0.1 / +0.2 % (profiles/r04_sgpr_ab.txt)
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(80))) k_generate(DevScene sc_g, rt_settings st, FrameParams fp, Pool pool,
                                                         Counters* cnt, int cur) {
-    // Once the partition is complete nothing is left to splat or claim (k_bookkeep sets done only
-    // when the last k_shade finished no path and continued none; the fused drain splats its own)
-    if (cnt->done) return;                          // uniform
     const uint32_t slot = blockIdx.x*blockDim.x + threadIdx.x;
     const uint32_t lane = __lane_id(), wave = (slot >> 6) & (uint32_t)(BLOCK / 64 - 1);   // wave in the group
     const uint32_t wbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)(slot >> 6));
@@ -2341,8 +2338,10 @@ __global__ void __launch_bounds__(BLOCK) RT_SHADE_ATTR k_shade(DevScene sc_g, rt
 // the re-runs splatted the poorer results over the finished records.  The default
 // schedule never ran into it only because every iteration after the first fused one carried the drain
 // kernels, whose fuse flag makes extend / shade / connect exit.  Now the drain leaves no live state
-// behind (and k_generate exits once Counters::done is set), whatever the host's cadence.  (A done
-// check in k_shade itself costs it an 8-byte spill at 64 VGPRs: the retired pool makes it unneeded.)
+// behind, whatever the host's cadence: a k_generate after it marks every slot S_FREE and claims
+// nothing (no sample is left), and the k_shade after that finds no path.  (A done check at the top of
+// k_shade costs it an 8-byte spill at 64 VGPRs, and one at the top of k_generate a dependent load
+// before its first: C3 -0.9 %, profiles/r06_vs_r05_ab.txt; the retired pool makes both unneeded.)
 __global__ void __launch_bounds__(BLOCK) k_drain_list(DevScene sc, rt_settings st, FrameParams fp, Pool pool, Counters* cnt,
                                                       int splat_prev) {
     if (!cnt->fused || cnt->done) return;                              // uniform
