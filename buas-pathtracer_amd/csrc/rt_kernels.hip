@@ -1884,7 +1884,8 @@ RT_D void trace_queue(const DevScene& sc, const Pool& pool, Counters* cnt, int c
 template <bool LST, bool REF, int PH>
 __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool pool, Counters* cnt, int cur, uint2* spill,
                                                               int fuse, uint32_t sh_pct) {
-    if (cnt->done) return;                          // uniform
+    // (no done check: once a partition is done its queues stay empty, and a check would put a dependent
+    // load in front of every block)
     // trace waves are latency bound and issue little; shade waves sharing the SIMD are
     // issue bound: let a trace wave's next load go out first (r03b, priority 1: a rank's share of 8
     // +0.4 to +1.6 % in five pairs, the full frames within noise; profiles/r03b_ab.txt section 23)
@@ -1898,8 +1899,8 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
     const bool ext = (PH & 1) && !(fuse && cnt->fused);
     __shared__ uint32_t qlen[2][NSHARD];
     if (threadIdx.x < NSHARD) {
-        qlen[0][threadIdx.x] = ext ? cnt->ext_count[cur][threadIdx.x][0] : 0u;
-        qlen[1][threadIdx.x] = cnt->shadow_count[cur ^ 1][threadIdx.x][0];
+        if (PH & 1) qlen[0][threadIdx.x] = ext ? cnt->ext_count[cur][threadIdx.x][0] : 0u;
+        if (PH & 2) qlen[1][threadIdx.x] = cnt->shadow_count[cur ^ 1][threadIdx.x][0];
     }
     __syncthreads();
     // the shadow queue after the extension items: sh_pct % of the blocks, spread evenly over the grid (and
