@@ -64,7 +64,7 @@ struct DevScene {
     uint32_t air_id;
     const rt_primitive* prims;
     const rt_primitive* planes;
-    const rt_primitive* planes_g;   // the planes in HBM, never rebased (the prologue's scalar loads)
+    const float4* plane_nd;         // the planes' p[0..3] (normal, distance) packed, padded to a multiple of 4 (the prologue's scalar loads)
     uint32_t plane_count;
     const M34* inv;                 // per transform: inverse (rows 0-2)
     const M34* fwd;                 // per transform: forward (rows 0-2)
@@ -112,7 +112,6 @@ struct DevScene {
 // scene_in_lds does not rebase them -- and its wave-uniform walk reads them with s_load
 // through the scalar cache: no LDS round trip and no readfirstlane per value
 // (ld_uniform's scalar load needs a global address).
-static_assert(sizeof(rt_primitive) == 32 && offsetof(rt_primitive, p) == 16, "the prologue loads a plane's p[] as one float4");
 enum { BLOB_MATERIALS, BLOB_PRIMS, BLOB_PLANES, BLOB_INV, BLOB_FWD, BLOB_LIGHTS, BLOB_MESHES, BLOB_COUNT };
 constexpr uint32_t LDS_SCENE_Q = 2048;   // 32 KB
 // The copy is the launch's dynamic LDS, sized to the blob (blob_q float4): a fixed
@@ -456,6 +455,27 @@ RT_D float4 ld_uniform(const float4* p) {
     const __attribute__((address_space(4))) float* f = reinterpret_cast<const __attribute__((address_space(4))) float*>(u);
     return make_float4(f[0], f[1], f[2], f[3]);
 }
+// The same for 8 or 16 consecutive dwords: one s_load_dwordx8 / x16.  Scalar loads return out of order,
+// so a wave waits for all of its outstanding ones (lgkmcnt(0)) before it uses any value: the prologue
+// fetches what a step needs in one batch rather than one float4 per wait.  The empty asm takes the whole
+// vector in SGPRs where it is loaded, so the compiler neither narrows it into per-field loads nor sinks
+// those into the branches that use them (each would be a wait of its own again).
+typedef float f32x8 __attribute__((ext_vector_type(8), aligned(16)));
+typedef float f32x16 __attribute__((ext_vector_type(16), aligned(16)));
+template <class V>
+RT_D V ld_uniform_v(const float4* p) {
+#ifdef __HIP_DEVICE_COMPILE__
+    if (__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p)) __builtin_trap();
+#endif
+    const uint64_t a = (uint64_t)p;
+    const uint64_t u = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32);
+    const V v = *reinterpret_cast<const __attribute__((address_space(4))) V*>(u);
+    asm volatile("" :: "s"(v));
+    return v;
+}
+RT_D float4 q4_of(const f32x16& v, int k) { return make_float4(v[4*k], v[4*k + 1], v[4*k + 2], v[4*k + 3]); }
+RT_D float4 q4_of(const f32x8& v, int k) { return make_float4(v[4*k], v[4*k + 1], v[4*k + 2], v[4*k + 3]); }
 constexpr uint32_t MLIST_FULL = 0xFFFFFFFFu;
 // calls: the mesh instances the walk reaches -- the top-level leaf holding one passes its pop-time
 // test, it is not the ignored light, and no plane, sphere or box has occluded a shadow query before
@@ -468,14 +488,20 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
     wr.zero = 0u;                                                  // no pruning on the world ray
     r.t = max_t; r.code = RT_HIT_MISS; r.occluded = false; r.bvh = false; r.inv_d = wr.inv_d; r.mlist = MLIST_FULL;
     r.calls = 0;
-    for (uint32_t i = 0; i < sc.plane_count; ++i) {
-        const float4 pl = ld_uniform(reinterpret_cast<const float4*>(sc.planes_g + i) + 1);   // p[0..3]
-        if (ray_plane(wr, {pl.x, pl.y, pl.z}, pl.w, r.t)) {
-            r.code = RT_HIT_PLANE_BIT | i;
-            if (occ) { r.occluded = true; return r; }
+    // four planes per batch; a lane whose shadow ray a plane occluded tests no further plane (the
+    // reference returns there, :424-433)
+    for (uint32_t i = 0; i < sc.plane_count; i += 4) {
+        const f32x16 pb = ld_uniform_v<f32x16>(sc.plane_nd + i);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+            const float4 pl = q4_of(pb, (int)k);
+            if (i + k < sc.plane_count && !r.occluded && ray_plane(wr, {pl.x, pl.y, pl.z}, pl.w, r.t)) {
+                r.code = RT_HIT_PLANE_BIT | (i + k);
+                if (occ) r.occluded = true;
+            }
         }
     }
-    if (!sc.bvh_node_count) return r;
+    if (r.occluded || !sc.bvh_node_count) return r;
     if (!sc.top_seq) {                                             // large top level: the kernel walks it
         const float4* q = reinterpret_cast<const float4*>(sc.bvh);
         const float4 a = q[0], b = q[1];
@@ -494,7 +520,8 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
     const uint32_t len = sc.top_seq_len;
     const bool plain = plain_ray(o, d);
     for (uint32_t i = 0; i < len; ++i) {
-        const float4 a = ld_uniform(seq + 2*i), b = ld_uniform(seq + 2*i + 1);
+        const f32x8 e = ld_uniform_v<f32x8>(seq + 2*i);
+        const float4 a = q4_of(e, 0), b = q4_of(e, 1);
         const uint32_t info = __float_as_uint(b.z), skip = __float_as_uint(b.w);
         bool pass = false;
         if (next == i) {
@@ -506,10 +533,11 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
         const uint32_t first = info & 0xFFFFFFu, end = first + ((info >> 24) & 127u);
         for (uint32_t j = first; j < end; ++j) {                   // the leaf's primitives in order
             const float4* q = sc.leaf_rec + (size_t)j*LEAF_REC_Q;
-            const float4 q3 = ld_uniform(q + 3);
+            const f32x16 qa = ld_uniform_v<f32x16>(q);                 // q0-q3
+            const float4 q3 = q4_of(qa, 3);
             const uint32_t pi = __float_as_uint(q3.x), tword = __float_as_uint(q3.y), type = tword & 0xFFu;
             if (!pass || pi == ignored) continue;
-            const float4 q0 = ld_uniform(q), q1 = ld_uniform(q + 1), q2 = ld_uniform(q + 2);
+            const float4 q0 = q4_of(qa, 0), q1 = q4_of(qa, 1), q2 = q4_of(qa, 2);
             V3 io, id;
             object_ray(q0, q1, q2, tword & LEAF_TRANSLATE, plain, o, d, io, id);   // transform_ray :403-409
             bool hit = false;
@@ -519,7 +547,8 @@ RT_D Prologue ray_prologue(const DevScene& sc, V3 o, V3 d, float max_t, bool occ
             } else {
                 const Ray ir = make_ray(io, id, 0.0f);
                 if (type == RT_PRIMITIVE_MESH) {                   // the mesh root's pop-time test (:269-275)
-                    const float4 q4 = ld_uniform(q + 4), q5 = ld_uniform(q + 5);
+                    const f32x8 qb = ld_uniform_v<f32x8>(q + 4);
+                    const float4 q4 = q4_of(qb, 0), q5 = q4_of(qb, 1);
                     float tm;
                     n += 1u << 8;                                  // intersect_mesh called (:488)
                     if (bv_static(ir, {q4.y, q4.z, q4.w}, {q5.x, q5.y, q5.z}, tm) && tm < r.t) {
@@ -4142,7 +4171,12 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         if (d->lights[i] >= d->primitive_count) { set_error("light id out of range"); return fail(RT_ERROR_INVALID); }
     if ((err = upload(s, d->primitives, d->primitive_count, &ds.prims))) return fail(err);
     if ((err = upload(s, d->planes, d->plane_count, &ds.planes))) return fail(err);
-    ds.planes_g = ds.planes;
+    {   // the prologue's plane table: p[0..3] per plane, four per scalar load
+        std::vector<float4> nd((d->plane_count + 3u) / 4u * 4u + 4u, make_float4(0, 0, 0, 0));
+        for (uint32_t i = 0; i < d->plane_count; ++i)
+            nd[i] = make_float4(d->planes[i].p[0], d->planes[i].p[1], d->planes[i].p[2], d->planes[i].p[3]);
+        if ((err = upload(s, nd.data(), nd.size(), &ds.plane_nd))) return fail(err);
+    }
     ds.plane_count = d->plane_count;
     std::vector<M34> inv(d->transform_count), fwd(d->transform_count);
     for (uint32_t i = 0; i < d->transform_count; ++i)
