@@ -1943,7 +1943,10 @@ __global__ void __launch_bounds__(TB) RT_TRACE_ATTR k_trace(DevScene sc, Pool po
 // k_shade — one bounce of advanced_integrator (RT/integrators.cpp:612-818)
 // 8 waves per SIMD (64 VGPRs) for the default instantiation (scene in LDS, no environment NEE),
 // which fits them without spills; the others need 66-67 and keep 7
-#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((IN_LDS && !ENV) ? 8 : 7)))
+#ifndef RT_SHADE_WAVES
+#define RT_SHADE_WAVES 8            // tuning builds: -DRT_SHADE_WAVES=7
+#endif
+#define RT_SHADE_ATTR __attribute__((amdgpu_waves_per_eu((IN_LDS && !ENV) ? RT_SHADE_WAVES : 7)))
 // One bounce of advanced_integrator (RT/integrators.cpp:612-815) for a path whose closest hit
 // is h: emission / MIS, Beer absorption, Fresnel, reflect / refract / diffuse with NEE (the
 // shadow ray is returned, not traced) and Russian roulette.  Shared by k_shade (one bounce per
