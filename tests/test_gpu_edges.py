@@ -86,6 +86,38 @@ def test_degenerate_scene_gpu_matches_oracle(rt, kind):
     _compare(rt, f"degenerate_{kind}", degenerate_scene(rt, kind), cam, st, fc, w, h)
 
 
+def plane_room(rt, n):
+    """A room of n planes (floor, ceiling, walls, then planes tilted outside it, each also tested by
+    every ray) with a sphere light and a glass sphere: the ray prologue loads the planes four per
+    scalar load (DevScene::plane_nd), so n = 4 fills one batch exactly and n = 9 ends in a partial one;
+    a shadow ray stops at the first plane that occludes it (RT/intersection.cpp:424-433)."""
+    s = rt.Scene()
+    m = [s.add_diffuse_material(c, 1.5) for c in ((0.6, 0.5, 0.4), (0.8, 0.2, 0.2), (0.2, 0.7, 0.3))]
+    glass = s.add_translucent_material((0.1, 0.1, 0.1), 1.5, 0.0)
+    light = s.add_emissive_material((9.0, 8.0, 7.0))
+    planes = [((0.0, 1.0, 0.0), -1.0), ((0.0, -1.0, 0.0), -6.0), ((1.0, 0.0, 0.0), -4.0), ((-1.0, 0.0, 0.0), -4.0),
+              ((0.0, 0.0, -1.0), -6.0), ((0.6, 0.8, 0.0), -9.0), ((-0.6, 0.0, 0.8), -9.0), ((0.0, -0.6, -0.8), -9.0),
+              ((0.48, 0.6, 0.64), -12.0)]
+    for i, (nrm, d) in enumerate(planes[:n]):
+        s.add_plane(m[i % 3], nrm, d)
+    s.add_sphere(light, 0.5, rt.translate((0.0, 4.5, 1.0)))
+    s.add_sphere(glass, 0.8, rt.translate((1.0, 0.0, 2.0)))
+    s.set_sky((0.6, 0.7, 0.9), (0.1, 0.1, 0.1))
+    s.create_scene_bvh()
+    return s
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [4, 9])
+def test_plane_batches_gpu_match_oracle(rt, n):
+    w, h = 48, 36
+    cam = _camera(rt, w, h, p=(0.0, 1.5, -3.0), at=(0.0, 1.0, 2.0))
+    st, _ = rt.default_settings()
+    st.samples_per_pixel = 8
+    fc = rt.load_reconstruction_kernel("Mitchell Netravali")
+    _compare(rt, f"plane_room_{n}", plane_room(rt, n), cam, st, fc, w, h)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,h", [(1, 1), (5, 3), (65, 33), (130, 7)])
 def test_ragged_frames_gpu_match_oracle(rt, w, h):
