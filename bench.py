@@ -206,7 +206,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--spp", type=int, default=0, help="override samples per pixel (0 = config's)")
     ap.add_argument("--width", type=int, default=0)
@@ -316,13 +316,22 @@ def main():
     wms = [0.0] * 6
     wl = [0] * 6                    # warm-up launches per stage, and the rays the trace stages got
     wtraced = [0, 0]
+    # The stage statistics cover the warm-up frames since the last change of the shadow launch: a whole
+    # frame's auto policy reads the scene's previous frame (rt_scene_config::shadow_launch), so a scene's
+    # first frame may trace its shadow rays in another launch than the frames after it.
+    nwf, wmode = 0, None
     for _ in range(args.warmup):
         s = step()
+        if s.shadow_launch != wmode:
+            wms, wl, wtraced, nwf, wmode = [0.0] * 6, [0] * 6, [0, 0], 0, s.shadow_launch
+        nwf += 1
         for k in range(6):
-            wms[k] += s.kernel_ms[k] / args.warmup
+            wms[k] += s.kernel_ms[k]
             wl[k] += s.kernel_launches[k]
         wtraced[0] += s.traced_rays[0]
         wtraced[1] += s.traced_rays[1]
+    if nwf:
+        wms = [x / nwf for x in wms]
     torch.cuda.synchronize(device)
     if args.warmup:
         dom_stage = max(range(5), key=lambda k: wms[k])
@@ -503,7 +512,7 @@ def main():
         # stage timed there; the frames are identical), against the L2 gather rate (MI355X_MICROARCH.md,
         # rows shared by every workgroup: 16.8-18.8 TB/s).  Reported for both trace kernels.
         traversal = None
-        if args.warmup:
+        if args.warmup and (wmode == rt.abi.RT_SHADOW_LAUNCH_MERGED) == merged:
             traversal = {"peak": L2_PEAK_GBS, "unit": "GB/s", "bytes_per_step": 128,
                          "source": "rt_stats::trace_steps of the timed frames (counted on the device; the trace launches' "
                                    "own steps, closest-hit and shadow, the fused drain's left out)",
@@ -518,7 +527,7 @@ def main():
                 k = STAGES.index(stage)
                 if not wl[k] or wms[k] <= 0 or not rays:
                     continue
-                launches = wl[k] / args.warmup                     # per frame
+                launches = wl[k] / nwf                             # per frame
                 steps = ksteps / args.steps                         # per frame
                 tb = 128.0 * steps / launches
                 mean_s = wms[k] / launches / 1e3

@@ -3185,6 +3185,9 @@ struct rt_scene {
     uint32_t drain_lanes_full = 0;  // k_drain lanes of a grid that fills the GPU (the fused-drain threshold's unit)
     uint32_t connect_grid = 0;      // the separate shadow launch's blocks (<= trace_grid: the spill area)
     uint32_t shadow_pct = 100;      // the k_trace blocks that also take the shadow queue, in % (RT_SHADOW_PCT)
+    // traced shadow rays per traced extension ray in this scene's last frame (-1: none yet): the
+    // shadow-launch policy's input (rt_scene_config::shadow_launch, AUTO)
+    double shadow_share = -1.0;
     float4* d_samp = nullptr;       // per-sample records for the deterministic splat
     float* d_samp_jy = nullptr;
     size_t samp_cap = 0;
@@ -3627,12 +3630,17 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     // launch, after its extension rays (one launch and one tail less per iteration; the finished paths are
     // splatted an iteration later).  Separate: a trace launch of their own after k_shade (r05's schedule).
     // Auto: merged for a rank's share of a multi-GPU frame and for small pools (under BK_LARGE_POOL), where
-    // an iteration is short and its launches' tails weigh most; separate for a whole frame on one GPU.  A/B
-    // (profiles/r06_shadow_launch_ab.txt), merged against separate: rank 0's C3 share of 8 32.8-33.0 ms against
-    // 34.1, of 4 61.7-61.9 against 62.7, of 2 116.4-117.0 against 117.9-119.1; the whole C3 frame within the
-    // box's noise; the whole C4 frame 174.8-175.5 against 171.6-171.7.
+    // an iteration is short and its launches' tails weigh most; for a whole frame on one GPU, merged when
+    // the scene's last frame traced at least SHADOW_SHARE_MERGED shadow rays per extension ray, else
+    // separate (a scene's first frame: separate).  A/B (profiles/r06_shadow_launch_ab.txt,
+    // r06_merged_whole_ab.txt), merged against separate: rank 0's C3 share of 8 32.8-33.0 ms against 34.1,
+    // of 4 61.7-61.9 against 62.7, of 2 116.4-117.0 against 117.9-119.1; whole frames after the batched
+    // prologue: C3 (0.26 shadow rays per extension ray) +0.7..+2.2 %, C2 (the same scene) +0.7..+2.3 %, C4
+    // (0.11) -1.1..-3.0 %.
+    constexpr double SHADOW_SHARE_MERGED = 0.15;
     const bool merged = s->cfg.shadow_launch == RT_SHADOW_LAUNCH_MERGED ||
-                        (s->cfg.shadow_launch == RT_SHADOW_LAUNCH_AUTO && (shard || pool_n < BK_LARGE_POOL));
+                        (s->cfg.shadow_launch == RT_SHADOW_LAUNCH_AUTO &&
+                         (shard || pool_n < BK_LARGE_POOL || s->shadow_share >= SHADOW_SHARE_MERGED));
     auto plan_of = [&](int k, uint32_t mode) {
         const Run& r = run[k];
         // merged: a path's record is written two iterations after its last bounce (its shadow ray rides in the
@@ -3869,6 +3877,7 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             for (int i = 0; i < 2*TV_N; ++i) tv[i] += c.trav[sh][i];
         iters = std::max(iters, run[k].iters);
     }
+    if (sum.traced_rays[0]) s->shadow_share = (double)sum.traced_rays[1] / (double)sum.traced_rays[0];
     // TraversalStats per kind (rt_stats::traversal, rt_abi.h)
     rt_traversal_stats ts[2] = {};
     uint64_t steps[2] = {};

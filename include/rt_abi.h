@@ -469,8 +469,10 @@ int rt_cancel(rt_scene* scene);
 /* rt_scene_config::shadow_launch (ABI 8): the shadow rays of an iteration's k_shade are traced in a launch
  * of their own right after it (SEPARATE), or in the next iteration's trace launch after its extension rays
  * (MERGED: one launch and one tail less per iteration; a finished path is splatted an iteration later).
- * AUTO: merged for a shard of a multi-rank frame (rt_tile_set::shard_count > 1) and for path pools under
- * 4M paths (small frames), separate for a whole frame on one GPU. */
+ * AUTO: merged for a shard of a multi-rank frame (rt_tile_set::shard_count > 1), for path pools under
+ * 4M paths (small frames), and for a whole frame on one GPU when the scene's previous frame traced at least
+ * 0.15 shadow rays per extension ray (rt_stats::traced_rays); else separate -- a scene's first whole frame
+ * is separate. */
 typedef enum rt_shadow_launch {
     RT_SHADOW_LAUNCH_AUTO = 0,
     RT_SHADOW_LAUNCH_SEPARATE = 1,

@@ -56,6 +56,11 @@ def test_full_frame_default_path(rt, preset, spp):
     dev = rt.DeviceScene(scene, 0)
     try:
         gpu, gs = dev.render(cam, st, fc, w, h)
+        # the auto shadow launch (rt_scene_config::shadow_launch): a scene's first whole frame traces its
+        # shadow rays in a launch of their own; later frames merge them into the trace launch when the
+        # last frame traced >= 0.15 shadow rays per extension ray (C2 / C3: ~0.26; C4: ~0.11) -- the
+        # bench's timed frames.  Both schedules trace the same rays; the frame is held to the same bar.
+        gpu2, gs2 = dev.render(cam, st, fc, w, h)
         rs = None
         if preset == "c3":         # the reference's own TraversalStats units (rt_scene_config::traversal_ref)
             with dev.configured(traversal_ref=1):
@@ -63,6 +68,12 @@ def test_full_frame_default_path(rt, preset, spp):
     finally:
         dev.close()
     assert gs.splat_mode == rt.abi.RT_SPLAT_STREAM
+    share = gs.traced_rays[1] / gs.traced_rays[0]
+    assert gs.shadow_launch == rt.abi.RT_SHADOW_LAUNCH_SEPARATE
+    assert gs2.shadow_launch == (rt.abi.RT_SHADOW_LAUNCH_MERGED if share >= 0.15 else rt.abi.RT_SHADOW_LAUNCH_SEPARATE)
+    assert gs2.shadow_launch == (rt.abi.RT_SHADOW_LAUNCH_SEPARATE if preset == "c4" else rt.abi.RT_SHADOW_LAUNCH_MERGED)
+    assert (gs.closest_hit_rays, gs.shadow_rays, tuple(gs.traced_rays)) == \
+        (gs2.closest_hit_rays, gs2.shadow_rays, tuple(gs2.traced_rays))
     threads = _threads()
     with ob.gpu_walk() as walk:
         cpu, cs = ob.render(scene.desc(), cam, st, fc, w, h, rng_mode=0, threads=threads)
@@ -72,11 +83,13 @@ def test_full_frame_default_path(rt, preset, spp):
         "rel_l2": err, "max_abs_weight_diff": float(np.abs(gpu[..., 3] - cpu[..., 3]).max()),
         "gpu_rays": [int(gs.closest_hit_rays), int(gs.shadow_rays)], "oracle_rays": [int(cs.closest_hit_rays), int(cs.shadow_rays)],
         "samples": int(gs.samples), "iterations": int(gs.iterations), "oracle_threads": threads,
+        "shadow_rays_per_extension_ray": share, "second_frame_shadow_launch": int(gs2.shadow_launch),
+        "second_frame_bitwise_equal": bool(np.array_equal(gpu, gpu2)), "second_frame_rel_l2": rel_l2(gpu2, cpu),
         "gpu_seconds": gs.seconds, "traversal": trav}
     assert gs.samples == cs.samples == w * h * spp
     assert (gs.closest_hit_rays, gs.shadow_rays) == (cs.closest_hit_rays, cs.shadow_rays)
     assert np.isfinite(gpu).all() and np.isfinite(cpu).all()
-    assert err <= 1e-5
+    assert err <= 1e-5 and rel_l2(gpu2, cpu) <= 1e-5
     check_traversal(gs, walk.result)
     if rs is not None:
         ref_report = check_traversal_ref(rs, cs)
