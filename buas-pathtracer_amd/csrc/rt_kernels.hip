@@ -3180,7 +3180,8 @@ struct rt_scene {
     size_t tiles_cap = 0;
     int32_t* d_tile_base = nullptr;
     size_t tile_base_cap = 0;
-    uint32_t trace_grid = 0;        // persistent k_trace blocks (extend)
+    uint32_t trace_grid = 0;        // persistent k_trace blocks (extend) for the largest pool (see run_frame)
+    bool grid_by_pool = true;       // RT_TRACE_GRID_BY_POOL: a smaller pool's trace launch takes fewer blocks
     uint32_t drain_grid = 0;        // persistent k_drain blocks (<= trace_grid: the spill area)
     uint32_t drain_lanes_full = 0;  // k_drain lanes of a grid that fills the GPU (the fused-drain threshold's unit)
     uint32_t connect_grid = 0;      // the separate shadow launch's blocks (<= trace_grid: the spill area)
@@ -3638,6 +3639,13 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     // prologue: C3 (0.26 shadow rays per extension ray) +0.7..+2.2 %, C2 (the same scene) +0.7..+2.3 %, C4
     // (0.11) -1.1..-3.0 %.
     constexpr double SHADOW_SHARE_MERGED = 0.15;
+    // The trace launch's grid: the scene's (RT_TRACE_GRID_PCT of one full-occupancy wave of blocks) is sized for
+    // a whole 1080p frame's pools; a small pool (under BK_LARGE_POOL: a rank's eighth of a multi-GPU frame,
+    // 3.3M paths) queues fewer rays per launch and takes two thirds of it, so the other partitions' kernels find
+    // the rest of the GPU sooner.  Rank 0's C3 share of 8 at 50 % of a wave instead of 75 %: +1.7..+3.3 % (3
+    // pairs); a grid by sqrt(pool / 8.4M) also gave a share of 4 (6.6M paths, 67 %) -0.6..0 %
+    // (profiles/r06_grid_by_pool_ab.txt).
+    const uint32_t tgrid = (s->grid_by_pool && pool_n < BK_LARGE_POOL) ? std::max(1u, s->trace_grid*2u/3u) : s->trace_grid;
     const bool merged = s->cfg.shadow_launch == RT_SHADOW_LAUNCH_MERGED ||
                         (s->cfg.shadow_launch == RT_SHADOW_LAUNCH_AUTO &&
                          (shard || pool_n < BK_LARGE_POOL || s->shadow_share >= SHADOW_SHARE_MERGED));
@@ -3709,8 +3717,8 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
             else if (ref) k_trace<false, true, PH><<<grid, TB, TRACE_LDS, q>>>(ds, tp, pt.cnt, tcur, pt.spill, fuse, shp);
             else k_trace<false, false, PH><<<grid, TB, TRACE_LDS, q>>>(ds, tp, pt.cnt, tcur, pt.spill, fuse, shp);
         };
-        if (merged) trace(std::integral_constant<int, 3>{}, pv, r.cur, s->trace_grid);
-        else trace(std::integral_constant<int, 1>{}, pv, r.cur, s->trace_grid);
+        if (merged) trace(std::integral_constant<int, 3>{}, pv, r.cur, tgrid);
+        else trace(std::integral_constant<int, 1>{}, pv, r.cur, tgrid);
         e(RT_KERNEL_EXTEND);
         if (fuse) {                      // the fused drain, after the shadow rays of the last k_shade are in
             k_drain_list<<<r.grid, BLOCK, 0, q>>>(ds, *st, fp, pv, pt.cnt, merged ? 1 : 0);
@@ -4455,6 +4463,9 @@ int rt_scene_upload(const rt_scene_desc* d, int device, rt_scene** out) {
         env_int("rt_scene_upload", "RT_SHADOW_PCT", 1, 100, shadow_pct, env_ok);
         s->shadow_pct = (uint32_t)shadow_pct;
         env_int("rt_scene_upload", "RT_DRAIN_GRID_PCT", 1, 100, drain_pct, env_ok);
+        long long by_pool = 1;
+        env_int("rt_scene_upload", "RT_TRACE_GRID_BY_POOL", 0, 1, by_pool, env_ok);
+        s->grid_by_pool = by_pool != 0;
         if (!env_ok) return fail(RT_ERROR_INVALID);
         const uint32_t full = s->trace_grid;
         s->trace_grid = std::max(1u, (uint32_t)((unsigned long long)full*(unsigned)grid_pct / 100ull));
