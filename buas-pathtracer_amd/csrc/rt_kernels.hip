@@ -3641,11 +3641,11 @@ int run_frame(rt_scene* s, const rt_settings* st, FrameParams fp, unsigned long 
     constexpr double SHADOW_SHARE_MERGED = 0.15;
     // The trace launch's grid: the scene's (RT_TRACE_GRID_PCT of one full-occupancy wave of blocks) is sized for
     // a whole 1080p frame's pools; a small pool (under BK_LARGE_POOL: a rank's eighth of a multi-GPU frame,
-    // 3.3M paths) queues fewer rays per launch and takes two thirds of it, so the other partitions' kernels find
-    // the rest of the GPU sooner.  Rank 0's C3 share of 8 at 50 % of a wave instead of 75 %: +1.7..+3.3 % (3
-    // pairs); a grid by sqrt(pool / 8.4M) also gave a share of 4 (6.6M paths, 67 %) -0.6..0 %
-    // (profiles/r06_grid_by_pool_ab.txt).
-    const uint32_t tgrid = (s->grid_by_pool && pool_n < BK_LARGE_POOL) ? std::max(1u, s->trace_grid*2u/3u) : s->trace_grid;
+    // 3.3M paths) queues fewer rays per launch and takes half of it, so the other partitions' kernels find the
+    // rest of the GPU sooner.  Rank 0's C3 share of 8 (profiles/r06_grid_by_pool_ab.txt): 50 % of a wave
+    // instead of 75 % +1.4..+3.3 %; then 37 % +0.4..+1.7 % and 31 % +0.1..+1.2 % over 50 %, 25 % -1.1..-2.0 %;
+    // a grid by sqrt(pool / 8.4M) also gave a share of 4 (6.6M paths, 67 %) -0.6..0 %.
+    const uint32_t tgrid = (s->grid_by_pool && pool_n < BK_LARGE_POOL) ? std::max(1u, s->trace_grid/2u) : s->trace_grid;
     const bool merged = s->cfg.shadow_launch == RT_SHADOW_LAUNCH_MERGED ||
                         (s->cfg.shadow_launch == RT_SHADOW_LAUNCH_AUTO &&
                          (shard || pool_n < BK_LARGE_POOL || s->shadow_share >= SHADOW_SHARE_MERGED));
